@@ -1,0 +1,68 @@
+"""Builds the native library libdpf_amd.so (HIP kernels for gfx950 + the C++
+host library + the C ABI) in-tree with hipcc.
+
+    python -m distributed_point_functions_amd.build_native [--force]
+"""
+from __future__ import annotations
+
+import concurrent.futures
+import glob
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+OUT_DIR = os.path.join(PKG, "_native")
+OBJ_DIR = os.path.join(OUT_DIR, "obj")
+LIB = os.path.join(OUT_DIR, "libdpf_amd.so")
+ARCH = os.environ.get("DPF_AMD_ARCH", "gfx950")
+
+CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+            "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
+
+
+def _sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) +
+                  glob.glob(os.path.join(CSRC, "*.cc")))
+
+
+def _headers_mtime():
+    hs = (glob.glob(os.path.join(CSRC, "*.h")) +
+          glob.glob(os.path.join(ROOT, "include", "*.h")) +
+          glob.glob(os.path.join(ROOT, "include", "dpf_amd", "*.h")))
+    return max([os.path.getmtime(h) for h in hs] + [0])
+
+
+def _compile(src: str, force: bool) -> str:
+    obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+    if (not force and os.path.exists(obj) and
+            os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime())):
+        return obj
+    cmd = ["hipcc"] + CXXFLAGS + ["-c", src, "-o", obj + ".tmp"]
+    if src.endswith(".hip"):
+        cmd[1:1] = ["--offload-arch=" + ARCH, "-x", "hip"]
+    else:
+        cmd[1:1] = ["-maes", "-msse4.1"]
+    subprocess.check_call(cmd)
+    os.replace(obj + ".tmp", obj)
+    return obj
+
+
+def build(force: bool = False, jobs: int = 8) -> str:
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    srcs = _sources()
+    with concurrent.futures.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+    if (force or not os.path.exists(LIB) or
+            os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs)):
+        tmp = LIB + ".tmp%d" % os.getpid()
+        subprocess.check_call(["hipcc", "--offload-arch=" + ARCH, "-shared", "-fPIC",
+                               "-o", tmp] + objs + ["-lpthread"])
+        os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))

@@ -1,0 +1,52 @@
+// internal.h — helpers shared by the HIP kernels and the C++ host library.
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+
+#include "aes_tables.h"
+#include "dpf_amd.h"
+
+namespace dpf_amd {
+
+// Thread-local error message for dpf_amd_last_error().
+int SetError(int code, const std::string& message);
+const char* LastError();
+
+// Device-side copy of dpf_amd_value_type plus everything the per-leaf
+// correction needs (kernel argument, < 2 KiB).
+constexpr int kMaxScalars = DPF_AMD_MAX_SCALARS;
+constexpr int kMaxCorrections = DPF_AMD_MAX_CORRECTIONS;
+
+struct alignas(16) ScalarDev {
+  int32_t kind;
+  int32_t bytes;
+  int32_t in_off;
+  int32_t out_off;
+  int32_t fold_w;    // IntModN fast reduction: m = 2^fold_w - fold_c
+  int32_t use_fold;  // 1 if the folding reduction is used
+  int32_t pad0, pad1;
+  u128 mod;
+  u128 fold_c;
+};
+
+struct alignas(16) VtDev {
+  int32_t ns;
+  int32_t direct;
+  int32_t epb;
+  int32_t esz;
+  int32_t bn;
+  int32_t stride;
+  int32_t cepb;
+  int32_t party;
+  ScalarDev sc[kMaxScalars];
+  u128 corr[kMaxCorrections];  // [element][scalar]
+  u128 corr_packed;  // single-scalar direct types: corrections packed like a block
+};
+
+// Fills the device descriptor; returns a status code.
+int MakeVtDev(const dpf_amd_value_type& vt, const uint64_t* correction,
+              int party, int cepb, VtDev* out);
+
+}  // namespace dpf_amd

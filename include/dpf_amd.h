@@ -1,0 +1,301 @@
+/*
+ * dpf_amd.h — C ABI of the MI355X-native DPF / dense-PIR hot path.
+ *
+ * Every entry point is `extern "C"`, takes plain pointers and sizes (no torch,
+ * no C++ types), and returns an int status equal to the absl::StatusCode
+ * number the reference would return (0 OK, 3 INVALID_ARGUMENT, 8
+ * RESOURCE_EXHAUSTED, 9 FAILED_PRECONDITION, 12 UNIMPLEMENTED, 13 INTERNAL).
+ * The message of the last failure on the calling thread is returned by
+ * dpf_amd_last_error().
+ *
+ * 128-bit integers (absl::uint128 in the reference) cross the ABI as two
+ * little-endian 64-bit words {lo, hi} — the in-memory layout of
+ * absl::uint128 / unsigned __int128 on x86-64 — so arrays of them are
+ * interchangeable with the reference's `absl::uint128*`.
+ *
+ * Two tiers:
+ *   Tier 1 (device pointers, stream-ordered): the internal seams of the
+ *     reference's hot path that the HIP kernels replace.  Inputs and outputs
+ *     live in HBM; `stream` is a hipStream_t (NULL = default stream).
+ *   Tier 2 (host memory, opaque handles): the reference's public objects
+ *     (DistributedPointFunction, EvaluationContext, DenseDpfPirServer) with
+ *     DpfKey / EvaluationContext / PirRequest / PirResponse exchanged in
+ *     protobuf wire format, exactly as a cgo / JNI / ctypes binding of the
+ *     reference would pass them.
+ * Reference file:line citations use the paths under /root/reference.
+ */
+#ifndef DPF_AMD_H_
+#define DPF_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPF_AMD_OK 0
+#define DPF_AMD_INVALID_ARGUMENT 3
+#define DPF_AMD_RESOURCE_EXHAUSTED 8
+#define DPF_AMD_FAILED_PRECONDITION 9
+#define DPF_AMD_UNIMPLEMENTED 12
+#define DPF_AMD_INTERNAL 13
+
+#define DPF_AMD_MAX_SCALARS 16
+#define DPF_AMD_MAX_CORRECTIONS 32
+#define DPF_AMD_MAX_BLOCKS_NEEDED 4
+
+/* Kinds are the proto field numbers of ValueType's oneof
+ * (dpf/distributed_point_function.proto:25-60). */
+#define DPF_AMD_KIND_INTEGER 1
+#define DPF_AMD_KIND_INT_MOD_N 3
+#define DPF_AMD_KIND_XOR_WRAPPER 4
+
+/* One scalar of a (flattened) value type T. */
+typedef struct {
+  int32_t kind;        /* DPF_AMD_KIND_* */
+  int32_t bytes;       /* sizeof(scalar): 1, 2, 4, 8 or 16 */
+  int32_t in_offset;   /* byte offset inside one element when converted
+                          directly (ValueTypeHelper::DirectlyFromBytes) */
+  int32_t out_offset;  /* byte offset inside one host-layout T */
+  uint64_t modulus[2]; /* IntModN modulus {lo, hi}; 0 otherwise */
+} dpf_amd_scalar;
+
+/* Runtime description of the value type T of EvaluateUntil<T> /
+ * EvaluateAt<T> — the template parameter cannot cross a C ABI, so the host
+ * passes what the reference's header templates compute at compile time
+ * (h:816-862, vth:525-606).  Produced by dpf_amd_describe_value_type(). */
+typedef struct {
+  int32_t num_scalars;
+  int32_t directly_convertible; /* can_be_converted_directly_v<T> */
+  int32_t elements_per_block;   /* ElementsPerBlock<T>() */
+  int32_t element_size;         /* (TotalBitSize<T>() + 7) / 8 (direct only) */
+  int32_t blocks_needed;        /* ceil(BitsNeeded / 128) (cc:603-610) */
+  int32_t out_stride;           /* sizeof(T) in the host layout */
+  int32_t reserved[2];
+  dpf_amd_scalar scalars[DPF_AMD_MAX_SCALARS];
+} dpf_amd_value_type;
+
+const char* dpf_amd_last_error(void);
+
+/* Library / device info. */
+int dpf_amd_device_count(int* count);
+const char* dpf_amd_version(void);
+
+/* ------------------------------------------------------------------------ */
+/* Tier 1: device seams                                                     */
+/* ------------------------------------------------------------------------ */
+
+/* Replaces Aes128FixedKeyHash::Evaluate (dpf/aes_128_fixed_key_hash.h:52-53,
+ * .cc:57-98): out[i] = AES_key(sigma(in[i])) ^ sigma(in[i]),
+ * sigma(x) = (x.hi ^ x.lo, x.hi).  In-place safe. */
+int dpf_amd_aes128_mmo(uint64_t key_lo, uint64_t key_hi, const void* in,
+                       void* out, int64_t n, void* stream);
+
+/* Replaces dpf_internal::EvaluateSeeds (dpf/internal/evaluate_prg_hwy.h:70-77,
+ * .cc:638-658) with the same argument meaning; `prg_left`/`prg_right` are
+ * given by their 128-bit keys.  num_correction_words must be num_levels or
+ * num_levels * num_seeds (INVALID_ARGUMENT otherwise, .cc:647-652); with
+ * per-seed words, seed i at level l uses word l * num_seeds + i.  All arrays
+ * are device pointers; seeds_out / control_bits_out may alias the inputs. */
+int dpf_amd_evaluate_seeds(int64_t num_seeds, int num_levels,
+                           int64_t num_correction_words, const void* seeds_in,
+                           const uint8_t* control_bits_in, const void* paths,
+                           int paths_rightshift, const void* correction_seeds,
+                           const uint8_t* correction_controls_left,
+                           const uint8_t* correction_controls_right,
+                           uint64_t key_left_lo, uint64_t key_left_hi,
+                           uint64_t key_right_lo, uint64_t key_right_hi,
+                           void* seeds_out, uint8_t* control_bits_out,
+                           void* stream);
+
+/* Fused ExpandSeeds (cc:289-372) + HashExpandedSeeds (cc:523-547) + the
+ * per-leaf value correction of EvaluateUntil (h:836-862), on a forest of
+ * `num_roots` roots each expanded `num_levels` tree levels with the DPF PRG
+ * keys (cc:55-60).  The concatenated leaf (tree block) index of root r,
+ * block j is g = r * 2^num_levels + j; leaves g in [leaf_begin, leaf_end)
+ * are produced, element e (< corrected_elements_per_block) of leaf g being
+ * written in host layout at
+ *   out + ((g - leaf_begin) * cepb + e) * vt->out_stride.
+ * Correction words for the num_levels levels are device arrays; the value
+ * correction (epb * num_scalars words of 128 bits, flattened per element)
+ * and the party are host values (h:815-827, 856-858). */
+int dpf_amd_expand_and_correct(
+    int64_t num_roots, const void* root_seeds, const uint8_t* root_control_bits,
+    int num_levels, const void* correction_seeds,
+    const uint8_t* correction_controls_left,
+    const uint8_t* correction_controls_right, const dpf_amd_value_type* vt,
+    const uint64_t* value_correction, int party,
+    int corrected_elements_per_block, int64_t leaf_begin, int64_t leaf_end,
+    void* out, void* stream);
+
+/* Fused single-path evaluation: EvaluateSeeds from the given seeds along
+ * `paths` (one AES per level, per-lane key select) + HashExpandedSeeds +
+ * correction of element block_index[i] (EvaluateAtImpl h:1013-1063 and the
+ * per-key loop of EvaluateAndApply h:1143-1189).  Per-seed arrays:
+ * seeds, control_bits, paths, block_index (may be NULL = 0), party (NULL =
+ * `party_all`), value_corrections (NULL = `value_correction_all`, else
+ * num_seeds * epb * num_scalars words).  Correction words are shared
+ * (num_cw == num_levels) or per seed (num_levels * num_seeds).  Writes one
+ * host-layout T per seed, and optionally the final seeds / control bits. */
+int dpf_amd_evaluate_points(
+    int64_t num_seeds, const void* seeds, const uint8_t* control_bits,
+    const void* paths, int paths_rightshift, int num_levels,
+    int64_t num_correction_words, const void* correction_seeds,
+    const uint8_t* correction_controls_left,
+    const uint8_t* correction_controls_right, const dpf_amd_value_type* vt,
+    const uint8_t* block_index, const int8_t* party, int party_all,
+    const void* value_corrections, const uint64_t* value_correction_all,
+    void* out, void* seeds_out, uint8_t* control_bits_out, void* stream);
+
+/* Gathers the per-prefix output slices of an incremental evaluation
+ * (h:877-889): out[i * opp + k] = in[src_offset[i] + k] for k < opp, rows of
+ * `stride` bytes. */
+int dpf_amd_gather_rows(int64_t num_prefixes, const int64_t* src_offset,
+                        int64_t outputs_per_prefix, int64_t stride,
+                        const void* in, void* out, void* stream);
+
+/* Replaces pir_internal::InnerProduct (pir/internal/inner_product_hwy.h:
+ * 38-41) for a database stored with a fixed, 16-byte-aligned record stride:
+ * for query q, out[q] = XOR of records r < num_records whose selection bit
+ * (bit r % 128 of 128-bit block r / 128 of selections[q]) is set.
+ * `selections` holds num_queries * selection_blocks 128-bit blocks,
+ * `out` num_queries * record_stride bytes.  `workspace` must hold
+ * dpf_amd_inner_product_workspace_size() bytes.  The scan reads every record
+ * exactly once with 16-byte loads and applies selections with masks
+ * (constant-time; no data-dependent skipping). */
+int64_t dpf_amd_inner_product_workspace_size(int64_t num_records,
+                                             int64_t record_stride,
+                                             int num_queries);
+int dpf_amd_inner_product(const void* db, int64_t num_records,
+                          int64_t record_stride, const void* selections,
+                          int64_t selection_blocks, int num_queries,
+                          void* workspace, void* out, void* stream);
+
+/* XOR-folds `num_parts` buffers of `bytes` bytes each (parts contiguous) into
+ * out — the local fold after an RCCL all-gather of XOR shares (RCCL has no
+ * XOR reduction). */
+int dpf_amd_xor_fold(const void* parts, int num_parts, int64_t bytes,
+                     void* out, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Tier 2: reference objects behind opaque handles (host memory)            */
+/* ------------------------------------------------------------------------ */
+
+typedef struct dpf_amd_dpf dpf_amd_dpf;
+typedef struct dpf_amd_ctx dpf_amd_ctx;
+typedef struct dpf_amd_pir_db dpf_amd_pir_db;
+typedef struct dpf_amd_pir_server dpf_amd_pir_server;
+
+/* Frees a buffer returned by this library (serialized protos). */
+void dpf_amd_free(void* p);
+
+/* Fills `vt` (layout + conversion metadata for T) from a serialized
+ * ValueType proto and a security parameter (which decides blocks_needed). */
+int dpf_amd_describe_value_type(const uint8_t* value_type_proto, size_t len,
+                                double security_parameter,
+                                dpf_amd_value_type* vt);
+
+/* DistributedPointFunction::CreateIncremental (h:102-103, cc:589-640);
+ * each parameters[i] is a serialized DpfParameters proto. */
+int dpf_amd_dpf_create_incremental(const uint8_t* const* parameters,
+                                   const size_t* lengths, int num_parameters,
+                                   dpf_amd_dpf** out);
+void dpf_amd_dpf_destroy(dpf_amd_dpf* dpf);
+/* Hierarchy metadata (proto_validator.cc:127-153). */
+int dpf_amd_dpf_tree_levels_needed(const dpf_amd_dpf* dpf);
+int dpf_amd_dpf_hierarchy_to_tree(const dpf_amd_dpf* dpf, int level);
+/* Output element type of hierarchy level `level`. */
+int dpf_amd_dpf_value_type(const dpf_amd_dpf* dpf, int level,
+                           dpf_amd_value_type* vt);
+
+/* GenerateKeysIncremental (h:258-259, cc:642-710).  betas[i] is a serialized
+ * Value proto for level i.  If `seeds` is non-NULL it supplies the two root
+ * seeds (4 words) instead of the CSPRNG (for reproducible fixtures only).
+ * Keys are returned as serialized DpfKey protos (free with dpf_amd_free). */
+int dpf_amd_dpf_generate_keys(dpf_amd_dpf* dpf, uint64_t alpha_lo,
+                              uint64_t alpha_hi, const uint8_t* const* betas,
+                              const size_t* beta_lengths,
+                              const uint64_t* seeds, uint8_t** key0,
+                              size_t* key0_len, uint8_t** key1,
+                              size_t* key1_len);
+
+/* CreateEvaluationContext (h:278, cc:712-727) from a serialized DpfKey. */
+int dpf_amd_ctx_create(const dpf_amd_dpf* dpf, const uint8_t* key,
+                       size_t key_len, dpf_amd_ctx** out);
+/* Parses / serializes a whole EvaluationContext proto. */
+int dpf_amd_ctx_parse(const dpf_amd_dpf* dpf, const uint8_t* data, size_t len,
+                      dpf_amd_ctx** out);
+int dpf_amd_ctx_serialize(const dpf_amd_ctx* ctx, uint8_t** data, size_t* len);
+void dpf_amd_ctx_destroy(dpf_amd_ctx* ctx);
+int dpf_amd_ctx_previous_hierarchy_level(const dpf_amd_ctx* ctx);
+int dpf_amd_ctx_partial_evaluations_level(const dpf_amd_ctx* ctx);
+int64_t dpf_amd_ctx_num_partial_evaluations(const dpf_amd_ctx* ctx);
+
+/* EvaluateUntil<T> (h:319-322, 695-891).  `value_type` is the serialized
+ * ValueType of T (checked as in h:709-716).  Writes host-layout T values to
+ * `out` (capacity in bytes); *num_outputs receives the element count.  With
+ * out == NULL only *num_outputs is computed. */
+int dpf_amd_evaluate_until(const dpf_amd_dpf* dpf, int hierarchy_level,
+                           const uint64_t* prefixes, int64_t num_prefixes,
+                           const uint8_t* value_type, size_t value_type_len,
+                           dpf_amd_ctx* ctx, void* out, int64_t out_capacity,
+                           int64_t* num_outputs);
+
+/* EvaluateAt<T>(key, level, points) (h:349-354, 913-1070). */
+int dpf_amd_evaluate_at(const dpf_amd_dpf* dpf, const uint8_t* key,
+                        size_t key_len, int hierarchy_level,
+                        const uint64_t* points, int64_t num_points,
+                        const uint8_t* value_type, size_t value_type_len,
+                        void* out);
+
+/* EvaluateAndApply<T, Fn> (h:403-407, 1072-1198) without the callback:
+ * evaluates key i at point i for every hierarchy level and writes
+ * num_levels * num_keys host-layout T values (level-major) to `out`. */
+int dpf_amd_evaluate_and_apply(const dpf_amd_dpf* dpf,
+                               const uint8_t* const* keys,
+                               const size_t* key_lengths, int64_t num_keys,
+                               const uint64_t* points, int rightshift,
+                               const uint8_t* value_type,
+                               size_t value_type_len, void* out);
+
+/* Dense PIR database: DenseDpfPirDatabase::Builder (pir/dense_dpf_pir_database.h
+ * :41-62) with the records resident in HBM. */
+int dpf_amd_pir_db_create(dpf_amd_pir_db** out);
+int dpf_amd_pir_db_insert(dpf_amd_pir_db* db, const uint8_t* record,
+                          size_t len);
+/* Bulk insert of num_records records of equal size. */
+int dpf_amd_pir_db_insert_fixed(dpf_amd_pir_db* db, const uint8_t* records,
+                                int64_t num_records, int64_t record_size);
+int dpf_amd_pir_db_build(dpf_amd_pir_db* db);
+void dpf_amd_pir_db_destroy(dpf_amd_pir_db* db);
+int64_t dpf_amd_pir_db_size(const dpf_amd_pir_db* db);
+int64_t dpf_amd_pir_db_max_value_size(const dpf_amd_pir_db* db);
+/* Device pointer / stride of the resident records (bench, multi-GPU). */
+const void* dpf_amd_pir_db_device_records(const dpf_amd_pir_db* db,
+                                          int64_t* record_stride);
+/* PirDatabaseInterface::InnerProductWith (pir/pir_database_interface.h:65-66):
+ * selections are host arrays of num_queries * selection_blocks 128-bit blocks;
+ * out receives num_queries * max_value_size bytes. */
+int dpf_amd_pir_db_inner_product(const dpf_amd_pir_db* db,
+                                 const uint64_t* selections,
+                                 int64_t selection_blocks, int num_queries,
+                                 uint8_t* out);
+
+/* DenseDpfPirServer::CreatePlain (pir/dense_dpf_pir_server.h:84-86) from a
+ * serialized PirConfig; takes ownership of `db`. */
+int dpf_amd_pir_server_create_plain(const uint8_t* config, size_t config_len,
+                                    dpf_amd_pir_db* db,
+                                    dpf_amd_pir_server** out);
+void dpf_amd_pir_server_destroy(dpf_amd_pir_server* server);
+/* DpfPirServer::HandleRequest (pir/dpf_pir_server.h:123-124): serialized
+ * PirRequest in, serialized PirResponse out. */
+int dpf_amd_pir_server_handle_request(const dpf_amd_pir_server* server,
+                                      const uint8_t* request,
+                                      size_t request_len, uint8_t** response,
+                                      size_t* response_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
