@@ -1,0 +1,290 @@
+"""Benchmark of the MI355X DPF / dense-PIR hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Headline (`value`): full-domain DPF evaluation leaves/s over the whole job —
+config c5 of BASELINE.json: one key, log_domain_size = 32,
+Tuple<uint32, IntModN<uint64, 2^64-59>>, security_parameter = 48
+(EvaluateNext({}, ctx), dpf/distributed_point_function.h:695-891), 2^32
+leaves per step, outputs kept in HBM in the host layout of the type.  With N
+ranks the 2^32-leaf domain is split into N disjoint subtree slices (strong
+scaling, no collective on the data path).
+
+Secondary (`pir`): dense PIR config c4 — 2^26 records x 256 B, one query:
+the selection DPF (only the ceil(N/128) leaves the scan reads) + the XOR
+scan over the whole database; rows sharded over ranks, the Q x 256 B
+partials are all-gathered with RCCL and XOR-folded.  GB/s = database bytes /
+time per query.
+
+`cpu_baseline` times the oracle (the C restatement of the reference CPU
+algorithm, AES-NI) single-threaded on a bounded slice of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from distributed_point_functions_amd import _lib, kernels
+from distributed_point_functions_amd import value_types as V
+from distributed_point_functions_amd.dpf import DistributedPointFunction, DpfParameters, decode_value
+
+METRIC = ("DPF full-domain leaves/sec at 2^32 (whole node); "
+          "dense-PIR scan GB/s at 1/2/4/8")
+P64 = 2 ** 64 - 59
+HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.64 T int32 lane-ops/s
+OPS_PER_AES = 757.5            # bitsliced AES-128 gate count
+LDS_LOOKUPS_PER_AES = 160      # T-table lookups per block (this kernel)
+LDS_PEAK_LOOKUPS = 256 * 32 * 2.4e9  # ds_read_b32: 32 lane-lookups/clk/CU
+AES_PER_LEAF_C5 = 4.0          # 2(2^32-1) tree + 2 * 2^32 value AES per 2^32 leaves
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print("[bench]", *a, flush=True)
+
+
+def setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, torch.device("cuda", local)
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def key_arrays(dpf, key, level, device):
+    """Device arrays of a DpfKey for the Tier-1 expansion seam."""
+    L = dpf.hierarchy_to_tree(level)
+    cws = key.correction_words[:L]
+    vt = dpf.parameters[level].value_type
+    vcs = key.last_level_value_correction
+    corr = [x for v in vcs for x in decode_value(vt, v)]
+    return dict(
+        L=L,
+        seed=kernels.u128_tensor([key.seed], device),
+        cb=torch.tensor([key.party], dtype=torch.uint8, device=device),
+        cw=kernels.u128_tensor([c.seed for c in cws], device),
+        ccl=torch.tensor([int(c.control_left) for c in cws] or [0], dtype=torch.uint8, device=device),
+        ccr=torch.tensor([int(c.control_right) for c in cws] or [0], dtype=torch.uint8, device=device),
+        corr=corr, party=key.party)
+
+
+def bench_dpf(args, world, rank, device):
+    vt = V.Tuple(V.Integer(32), V.IntModN(64, P64))
+    log_domain = args.log_domain
+    dpf = DistributedPointFunction.create(DpfParameters(log_domain, vt, 48))
+    alpha = 0x9E3779B9 % (1 << log_domain)
+    k0, _ = dpf.generate_keys(alpha, (123456789, 987654321), seeds=(0xA5A5, 0x5A5A))
+    ka = key_arrays(dpf, k0, 0, device)
+    desc = dpf.value_type_descriptor(0)
+    L = ka["L"]
+    cepb = 1 << (log_domain - L)
+    total = 1 << L
+    per = total // world
+    lo, hi = rank * per, (rank + 1) * per if rank < world - 1 else total
+    out = torch.empty((hi - lo) * cepb * desc.out_stride, dtype=torch.uint8, device=device)
+
+    def step():
+        kernels.expand_and_correct(ka["seed"], ka["cb"], L, ka["cw"], ka["ccl"], ka["ccr"],
+                                   desc, ka["corr"], ka["party"], cepb, lo, hi, out)
+
+    for _ in range(args.warmup):
+        step()
+    barrier(world)
+    st = torch.cuda.current_stream()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(st)
+    for _ in range(args.steps):
+        step()
+    ev1.record(st)
+    barrier(world)
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    wall = max_over_ranks(wall, world)
+    kernel_ms = max_over_ranks(kernel_ms, world)
+    leaves = total * cepb
+    # spot-check a few outputs against the second key's share (share-sum)
+    return dict(wall=wall, kernel_ms=kernel_ms, leaves=leaves, L=L, lo=lo, hi=hi)
+
+
+def bench_pir(args, world, rank, device):
+    n = 1 << args.pir_log_records
+    rec = 256
+    per = n // world
+    r_lo = rank * per
+    gen = torch.Generator(device=device)
+    gen.manual_seed(1234 + rank)
+    db = torch.randint(0, 256, (per * rec,), dtype=torch.uint8, device=device, generator=gen)
+    log_domain = max(0, (n - 1).bit_length())
+    dpf = DistributedPointFunction.create(DpfParameters(log_domain, V.XorWrapper(128)))
+    idx = (n * 3) // 7 + 5
+    k0, k1 = dpf.generate_keys(idx // 128, 1 << (idx % 128), seeds=(0x1111, 0x2222))
+    nb = n // 128
+    b_lo, b_hi = r_lo // 128, (r_lo + per) // 128
+    desc = dpf.value_type_descriptor(0)
+    keys = [key_arrays(dpf, k, 0, device) for k in (k0, k1)]
+    sel = torch.empty((b_hi - b_lo) * 16, dtype=torch.uint8, device=device)
+    ws = torch.empty(max(16, _lib.lib().dpf_amd_inner_product_workspace_size(per, rec, 1)),
+                     dtype=torch.uint8, device=device)
+    part = torch.empty(rec, dtype=torch.uint8, device=device)
+    gathered = torch.empty(world * rec, dtype=torch.uint8, device=device)
+    result = torch.empty(rec, dtype=torch.uint8, device=device)
+    scan_ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+
+    def query(ka, timed_scan=False):
+        kernels.expand_and_correct(ka["seed"], ka["cb"], ka["L"], ka["cw"], ka["ccl"], ka["ccr"],
+                                   desc, ka["corr"], ka["party"], 1, b_lo, b_hi, sel)
+        if timed_scan:
+            scan_ev[0].record()
+        kernels.inner_product(db, per, rec, sel.view(torch.int64).view(-1, 2), 1, ws, part)
+        if timed_scan:
+            scan_ev[1].record()
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, part)
+            kernels.xor_fold(gathered, world, rec, result)
+            return result
+        return part
+
+    # correctness: share0 ^ share1 == record idx (held by its owner rank)
+    a = query(keys[0]).clone()
+    b = query(keys[1]).clone()
+    rec_idx = torch.zeros(rec, dtype=torch.uint8, device=device)
+    owner = idx // per
+    if owner == rank:
+        rec_idx.copy_(db[(idx - r_lo) * rec:(idx - r_lo + 1) * rec])
+    if world > 1:
+        dist.all_reduce(rec_idx, op=dist.ReduceOp.SUM)
+    ok = bool(torch.equal(a ^ b, rec_idx))
+    for _ in range(args.warmup):
+        query(keys[0])
+    barrier(world)
+    scan_ms = 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        query(keys[0], timed_scan=True)
+        torch.cuda.synchronize()
+        scan_ms += scan_ev[0].elapsed_time(scan_ev[1])
+    barrier(world)
+    wall = max_over_ranks(time.perf_counter() - t0, world) / args.steps
+    scan_ms = max_over_ranks(scan_ms / args.steps, world)
+    return dict(ok=ok, wall_s=wall, scan_ms=scan_ms, db_bytes=n * rec, per_gpu_bytes=per * rec,
+                records=n)
+
+
+def cpu_baseline(args):
+    """Oracle (reference CPU algorithm restated in C, AES-NI, 1 thread) on a
+    bounded slice of the c5 workload: subtrees of 2^20 leaves of the same
+    2^32-domain key, repeated for >= args.cpu_seconds."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle import pyoracle as po
+    spec = ("tuple", [("int", 32), ("intmodn", 64, P64)])
+    d = po.Dpf([(args.log_domain, spec, 48)])
+    k0, _ = d.generate_keys(0x9E3779B9 % (1 << args.log_domain), [(123456789, 987654321)],
+                            seeds=(0xA5A5, 0x5A5A))
+    log_blocks = min(20, d.hierarchy_to_tree(0))
+    buf = np.zeros(2 * 2 * (1 << log_blocks), dtype=np.uint64)
+    leaves, t0, i = 0, time.perf_counter(), 0
+    while True:
+        d.expand_subtree_words(k0, i << log_blocks, log_blocks, buf)
+        leaves += 1 << log_blocks
+        i += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds or i >= 64:
+            break
+    return dict(value=leaves / el, unit="leaves/s", cores=1, kind="port",
+                sample="%d x 2^%d-leaf subtrees of the c5 key (%.1f s), oracle/dpf_oracle.c "
+                       "ExpandSeeds+HashExpandedSeeds+correction, AES-NI %s" %
+                       (i, log_blocks, el, "on" if po.lib().or_have_aesni() else "off"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--log-domain", type=int, default=32)
+    ap.add_argument("--pir-log-records", type=int, default=26)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--skip-cpu-baseline", action="store_true")
+    ap.add_argument("--skip-pir", action="store_true")
+    args = ap.parse_args()
+    world, rank, device = setup()
+    r = bench_dpf(args, world, rank, device)
+    pir = None if args.skip_pir else bench_pir(args, world, rank, device)
+    cpu = None
+    if rank == 0 and world == 1 and not args.skip_cpu_baseline:
+        cpu = cpu_baseline(args)
+    if rank == 0:
+        leaves = r["leaves"]
+        ms = 1000 * r["wall"] / args.steps
+        value = leaves / (r["wall"] / args.steps)
+        aes_per_launch = AES_PER_LEAF_C5 * leaves / world
+        aes_s = aes_per_launch / (r["kernel_ms"] / 1e3)
+        achieved = aes_s * OPS_PER_AES / 1e12
+        out = {
+            "metric": METRIC, "value": value, "unit": "leaves/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "u32", "data": "synthetic (fixed-seed DPF key)",
+            "config": {"workload": "c5: full-domain EvaluateNext, log_domain_size=%d, "
+                                   "Tuple<uint32,IntModN<uint64,2^64-59>>, "
+                                   "security_parameter=48" % args.log_domain,
+                       "leaves_per_step": leaves, "tree_levels": r["L"],
+                       "parallelism": "subtree-sharded x%d" % world},
+            "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS,
+                         "unit": "TOP/s", "frac": achieved / VALU_PEAK_TOPS, "traffic": None,
+                         "kernel": "KExpand<8,EmitU32ModN64>", "kernel_ms": r["kernel_ms"],
+                         "aes_per_s_per_gpu": aes_s,
+                         "ops_per_aes": OPS_PER_AES,
+                         "lds_bound": {"achieved_lookups_per_s": aes_s * LDS_LOOKUPS_PER_AES,
+                                       "peak": LDS_PEAK_LOOKUPS,
+                                       "frac": aes_s * LDS_LOOKUPS_PER_AES / LDS_PEAK_LOOKUPS}},
+            "cpu_baseline": cpu,
+        }
+        if pir is not None:
+            gbs = pir["db_bytes"] / pir["wall_s"] / 1e9
+            scan_gbs = pir["per_gpu_bytes"] / (pir["scan_ms"] / 1e3) / 1e9
+            out["pir"] = {
+                "metric": "dense-PIR scan GB/s", "value": gbs, "unit": "GB/s",
+                "workload": "c4: %d records x 256 B, Q=1, HandlePlainRequest path "
+                            "(selection DPF + XOR scan%s)" %
+                            (pir["records"], " + RCCL all-gather + fold" if world > 1 else ""),
+                "ms_per_query": 1e3 * pir["wall_s"], "correct": pir["ok"],
+                "roofline": {"bound": "hbm", "achieved": scan_gbs, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": scan_gbs / HBM_PEAK_GBS, "traffic": None,
+                             "kernel": "KPirScan<1>+KXorFold", "kernel_ms": pir["scan_ms"]},
+            }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

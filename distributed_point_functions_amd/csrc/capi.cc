@@ -1,0 +1,327 @@
+// capi.cc — Tier-2 C ABI (include/dpf_amd.h): the reference's public objects
+// behind opaque handles, with protos exchanged in wire format.
+#include <stdlib.h>
+#include <string.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "dpf_amd.h"
+#include "dpf_amd/dense_dpf_pir_server.h"
+#include "dpf_amd/distributed_point_function.h"
+#include "internal.h"
+
+using namespace distributed_point_functions;
+
+struct dpf_amd_dpf {
+  std::unique_ptr<DistributedPointFunction> dpf;
+};
+struct dpf_amd_ctx {
+  EvaluationContext ctx;
+};
+struct dpf_amd_pir_db {
+  std::unique_ptr<DenseDpfPirDatabase::Builder> builder =
+      std::make_unique<DenseDpfPirDatabase::Builder>();
+  std::unique_ptr<DenseDpfPirDatabase::Interface> built;
+  const DenseDpfPirDatabase* gpu() const {
+    return dynamic_cast<const DenseDpfPirDatabase*>(built.get());
+  }
+};
+struct dpf_amd_pir_server {
+  std::unique_ptr<DenseDpfPirServer> server;
+};
+
+namespace distributed_point_functions {
+namespace dpf_internal {
+StatusOr<std::unique_ptr<class DpfState>> MakeDpfState(Span<const DpfParameters>);
+}
+}  // namespace distributed_point_functions
+
+namespace {
+
+int Fail(const Status& s) { return dpf_amd::SetError(s.raw_code(), s.message()); }
+int Fail(int code, const std::string& m) { return dpf_amd::SetError(code, m); }
+
+int ToBuffer(const std::string& s, uint8_t** out, size_t* len) {
+  *out = static_cast<uint8_t*>(malloc(s.size() ? s.size() : 1));
+  if (!*out) return Fail(DPF_AMD_RESOURCE_EXHAUSTED, "malloc failed");
+  if (!s.empty()) memcpy(*out, s.data(), s.size());
+  *len = s.size();
+  return DPF_AMD_OK;
+}
+
+std::vector<uint128> ToU128(const uint64_t* w, int64_t n) {
+  std::vector<uint128> r(n);
+  for (int64_t i = 0; i < n; ++i) r[i] = MakeUint128(w[2 * i + 1], w[2 * i]);
+  return r;
+}
+
+int ParseType(const uint8_t* p, size_t n, ValueType* vt) {
+  if (!ParseValueType(p, n, vt)) return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed ValueType proto");
+  return DPF_AMD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dpf_amd_describe_value_type(const uint8_t* value_type_proto, size_t len,
+                                double security_parameter, dpf_amd_value_type* vt) {
+  DpfParameters p;
+  if (!ParseValueType(value_type_proto, len, p.mutable_value_type()))
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed ValueType proto");
+  p.set_security_parameter(security_parameter);
+  StatusOr<std::unique_ptr<DistributedPointFunction>> d = DistributedPointFunction::Create(p);
+  if (!d.ok()) return Fail(d.status());
+  *vt = (*d)->value_type_descriptor(0);
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_dpf_create_incremental(const uint8_t* const* parameters, const size_t* lengths,
+                                   int num_parameters, dpf_amd_dpf** out) {
+  std::vector<DpfParameters> ps(num_parameters > 0 ? num_parameters : 0);
+  for (int i = 0; i < num_parameters; ++i)
+    if (!ParseDpfParameters(parameters[i], lengths[i], &ps[i]))
+      return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed DpfParameters proto");
+  StatusOr<std::unique_ptr<DistributedPointFunction>> d =
+      DistributedPointFunction::CreateIncremental(Span<const DpfParameters>(ps.data(), ps.size()));
+  if (!d.ok()) return Fail(d.status());
+  *out = new dpf_amd_dpf{std::move(*d)};
+  return DPF_AMD_OK;
+}
+
+void dpf_amd_dpf_destroy(dpf_amd_dpf* dpf) { delete dpf; }
+
+int dpf_amd_dpf_tree_levels_needed(const dpf_amd_dpf* dpf) {
+  return dpf->dpf->tree_levels_needed();
+}
+int dpf_amd_dpf_hierarchy_to_tree(const dpf_amd_dpf* dpf, int level) {
+  return dpf->dpf->hierarchy_to_tree(level);
+}
+int dpf_amd_dpf_value_type(const dpf_amd_dpf* dpf, int level, dpf_amd_value_type* vt) {
+  if (level < 0 || level >= dpf->dpf->num_hierarchy_levels())
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "level out of range");
+  *vt = dpf->dpf->value_type_descriptor(level);
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_dpf_generate_keys(dpf_amd_dpf* dpf, uint64_t alpha_lo, uint64_t alpha_hi,
+                              const uint8_t* const* betas, const size_t* beta_lengths,
+                              const uint64_t* seeds, uint8_t** key0, size_t* key0_len,
+                              uint8_t** key1, size_t* key1_len) {
+  const int n = dpf->dpf->num_hierarchy_levels();
+  std::vector<Value> values(n);
+  for (int i = 0; i < n; ++i)
+    if (!ParseValue(betas[i], beta_lengths[i], &values[i]))
+      return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed Value proto");
+  const uint128 alpha = MakeUint128(alpha_hi, alpha_lo);
+  Span<const Value> span(values.data(), values.size());
+  StatusOr<std::pair<DpfKey, DpfKey>> keys =
+      seeds ? dpf->dpf->GenerateKeysIncrementalWithSeeds(alpha, span,
+                                                         MakeUint128(seeds[1], seeds[0]),
+                                                         MakeUint128(seeds[3], seeds[2]))
+            : dpf->dpf->GenerateKeysIncremental(alpha, span);
+  if (!keys.ok()) return Fail(keys.status());
+  int rc = ToBuffer(keys->first.SerializeAsString(), key0, key0_len);
+  if (rc != DPF_AMD_OK) return rc;
+  rc = ToBuffer(keys->second.SerializeAsString(), key1, key1_len);
+  if (rc != DPF_AMD_OK) free(*key0);
+  return rc;
+}
+
+int dpf_amd_ctx_create(const dpf_amd_dpf* dpf, const uint8_t* key, size_t key_len,
+                       dpf_amd_ctx** out) {
+  DpfKey k;
+  if (!k.ParseFromArray(key, key_len)) return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed DpfKey proto");
+  StatusOr<EvaluationContext> ctx = dpf->dpf->CreateEvaluationContext(std::move(k));
+  if (!ctx.ok()) return Fail(ctx.status());
+  *out = new dpf_amd_ctx{std::move(*ctx)};
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_ctx_parse(const dpf_amd_dpf* dpf, const uint8_t* data, size_t len,
+                      dpf_amd_ctx** out) {
+  (void)dpf;
+  auto c = std::make_unique<dpf_amd_ctx>();
+  if (!c->ctx.ParseFromArray(data, len))
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed EvaluationContext proto");
+  *out = c.release();
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_ctx_serialize(const dpf_amd_ctx* ctx, uint8_t** data, size_t* len) {
+  return ToBuffer(ctx->ctx.SerializeAsString(), data, len);
+}
+
+void dpf_amd_ctx_destroy(dpf_amd_ctx* ctx) { delete ctx; }
+int dpf_amd_ctx_previous_hierarchy_level(const dpf_amd_ctx* ctx) {
+  return ctx->ctx.previous_hierarchy_level();
+}
+int dpf_amd_ctx_partial_evaluations_level(const dpf_amd_ctx* ctx) {
+  return ctx->ctx.partial_evaluations_level();
+}
+int64_t dpf_amd_ctx_num_partial_evaluations(const dpf_amd_ctx* ctx) {
+  return ctx->ctx.partial_evaluations_size();
+}
+
+int dpf_amd_evaluate_until(const dpf_amd_dpf* dpf, int hierarchy_level,
+                           const uint64_t* prefixes, int64_t num_prefixes,
+                           const uint8_t* value_type, size_t value_type_len, dpf_amd_ctx* ctx,
+                           void* out, int64_t out_capacity, int64_t* num_outputs) {
+  ValueType t;
+  int rc = ParseType(value_type, value_type_len, &t);
+  if (rc != DPF_AMD_OK) return rc;
+  Status st = dpf->dpf->CheckType(t, hierarchy_level, false);
+  if (!st.ok()) return Fail(st);
+  std::vector<uint128> p = ToU128(prefixes, num_prefixes);
+  const int lvl = (hierarchy_level >= 0 && hierarchy_level < dpf->dpf->num_hierarchy_levels())
+                      ? hierarchy_level
+                      : 0;
+  const dpf_amd_value_type layout = dpf->dpf->value_type_descriptor(lvl);
+  const int64_t cap = layout.out_stride > 0 ? out_capacity / layout.out_stride : 0;
+  st = dpf->dpf->EvaluateUntilRaw(hierarchy_level, Span<const uint128>(p.data(), p.size()),
+                                  ctx->ctx, layout, out, cap, num_outputs, false, nullptr);
+  return st.ok() ? DPF_AMD_OK : Fail(st);
+}
+
+int dpf_amd_evaluate_at(const dpf_amd_dpf* dpf, const uint8_t* key, size_t key_len,
+                        int hierarchy_level, const uint64_t* points, int64_t num_points,
+                        const uint8_t* value_type, size_t value_type_len, void* out) {
+  DpfKey k;
+  if (!k.ParseFromArray(key, key_len)) return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed DpfKey proto");
+  ValueType t;
+  int rc = ParseType(value_type, value_type_len, &t);
+  if (rc != DPF_AMD_OK) return rc;
+  Status st = dpf->dpf->CheckType(t, hierarchy_level, true);
+  if (!st.ok()) return Fail(st);
+  std::vector<uint128> p = ToU128(points, num_points);
+  const int lvl = (hierarchy_level >= 0 && hierarchy_level < dpf->dpf->num_hierarchy_levels())
+                      ? hierarchy_level
+                      : 0;
+  st = dpf->dpf->EvaluateAtRaw(k, hierarchy_level, Span<const uint128>(p.data(), p.size()),
+                               nullptr, dpf->dpf->value_type_descriptor(lvl), out);
+  return st.ok() ? DPF_AMD_OK : Fail(st);
+}
+
+int dpf_amd_evaluate_and_apply(const dpf_amd_dpf* dpf, const uint8_t* const* keys,
+                               const size_t* key_lengths, int64_t num_keys,
+                               const uint64_t* points, int rightshift,
+                               const uint8_t* value_type, size_t value_type_len, void* out) {
+  std::vector<DpfKey> ks(num_keys);
+  std::vector<const DpfKey*> ptrs(num_keys);
+  for (int64_t i = 0; i < num_keys; ++i) {
+    if (!ks[i].ParseFromArray(keys[i], key_lengths[i]))
+      return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed DpfKey proto");
+    ptrs[i] = &ks[i];
+  }
+  ValueType t;
+  int rc = ParseType(value_type, value_type_len, &t);
+  if (rc != DPF_AMD_OK) return rc;
+  Status st = dpf->dpf->CheckType(t, -1, true);
+  if (!st.ok()) return Fail(st);
+  std::vector<uint128> p = ToU128(points, num_keys);
+  int done = 0;
+  st = dpf->dpf->EvaluateAndApplyRaw(Span<const DpfKey* const>(ptrs.data(), ptrs.size()),
+                                     Span<const uint128>(p.data(), p.size()), rightshift,
+                                     dpf->dpf->value_type_descriptor(0), out, &done);
+  return st.ok() ? DPF_AMD_OK : Fail(st);
+}
+
+// --- PIR ---------------------------------------------------------------------
+
+int dpf_amd_pir_db_create(dpf_amd_pir_db** out) {
+  *out = new dpf_amd_pir_db();
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_pir_db_insert(dpf_amd_pir_db* db, const uint8_t* record, size_t len) {
+  if (!db->builder) return Fail(DPF_AMD_FAILED_PRECONDITION, "Database already built");
+  db->builder->Insert(std::string(reinterpret_cast<const char*>(record), len));
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_pir_db_insert_fixed(dpf_amd_pir_db* db, const uint8_t* records, int64_t num_records,
+                                int64_t record_size) {
+  if (!db->builder) return Fail(DPF_AMD_FAILED_PRECONDITION, "Database already built");
+  db->builder->InsertFixed(reinterpret_cast<const char*>(records), num_records, record_size);
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_pir_db_build(dpf_amd_pir_db* db) {
+  if (!db->builder) return Fail(DPF_AMD_FAILED_PRECONDITION, "Database already built");
+  StatusOr<std::unique_ptr<DenseDpfPirDatabase::Interface>> b = db->builder->Build();
+  if (!b.ok()) return Fail(b.status());
+  db->built = std::move(*b);
+  db->builder.reset();
+  return DPF_AMD_OK;
+}
+
+void dpf_amd_pir_db_destroy(dpf_amd_pir_db* db) { delete db; }
+
+int64_t dpf_amd_pir_db_size(const dpf_amd_pir_db* db) {
+  return db->built ? static_cast<int64_t>(db->built->size()) : 0;
+}
+int64_t dpf_amd_pir_db_max_value_size(const dpf_amd_pir_db* db) {
+  return db->gpu() ? static_cast<int64_t>(db->gpu()->max_value_size_in_bytes()) : 0;
+}
+const void* dpf_amd_pir_db_device_records(const dpf_amd_pir_db* db, int64_t* record_stride) {
+  if (!db->gpu()) return nullptr;
+  *record_stride = db->gpu()->record_stride();
+  return db->gpu()->device_records();
+}
+
+int dpf_amd_pir_db_inner_product(const dpf_amd_pir_db* db, const uint64_t* selections,
+                                 int64_t selection_blocks, int num_queries, uint8_t* out) {
+  if (!db->gpu()) return Fail(DPF_AMD_FAILED_PRECONDITION, "database not built");
+  std::vector<std::vector<XorWrapper<uint128>>> sel(num_queries);
+  for (int q = 0; q < num_queries; ++q) {
+    sel[q].resize(selection_blocks);
+    for (int64_t b = 0; b < selection_blocks; ++b) {
+      const uint64_t* w = selections + 2 * (q * selection_blocks + b);
+      sel[q][b] = XorWrapper<uint128>(MakeUint128(w[1], w[0]));
+    }
+  }
+  StatusOr<std::vector<std::string>> r = db->built->InnerProductWith(
+      Span<const std::vector<XorWrapper<uint128>>>(sel.data(), sel.size()));
+  if (!r.ok()) return Fail(r.status());
+  size_t off = 0;
+  for (const std::string& s : *r) {
+    memcpy(out + off, s.data(), s.size());
+    off += s.size();
+  }
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_pir_server_create_plain(const uint8_t* config, size_t config_len, dpf_amd_pir_db* db,
+                                    dpf_amd_pir_server** out) {
+  PirConfig c;
+  if (!c.ParseFromArray(config, config_len))
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed PirConfig proto");
+  if (db && !db->built) {
+    int rc = dpf_amd_pir_db_build(db);
+    if (rc != DPF_AMD_OK) return rc;
+  }
+  std::unique_ptr<DenseDpfPirServer::Database> d;
+  if (db) d = std::move(db->built);
+  StatusOr<std::unique_ptr<DenseDpfPirServer>> s = DenseDpfPirServer::CreatePlain(c, std::move(d));
+  delete db;
+  if (!s.ok()) return Fail(s.status());
+  *out = new dpf_amd_pir_server{std::move(*s)};
+  return DPF_AMD_OK;
+}
+
+void dpf_amd_pir_server_destroy(dpf_amd_pir_server* server) { delete server; }
+
+int dpf_amd_pir_server_handle_request(const dpf_amd_pir_server* server, const uint8_t* request,
+                                      size_t request_len, uint8_t** response,
+                                      size_t* response_len) {
+  PirRequest r;
+  if (!r.ParseFromArray(request, request_len))
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed PirRequest proto");
+  StatusOr<PirResponse> resp = server->server->HandleRequest(r);
+  if (!resp.ok()) return Fail(resp.status());
+  return ToBuffer(resp->SerializeAsString(), response, response_len);
+}
+
+}  // extern "C"

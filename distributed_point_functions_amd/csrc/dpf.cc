@@ -1,0 +1,1404 @@
+// dpf.cc — DistributedPointFunction on MI355X.
+//
+// Host side (as in the reference): parameter / key / context validation
+// (dpf/internal/proto_validator.cc), BitsNeeded and value algebra
+// (dpf/internal/value_type_helpers.{h,cc}, dpf/int_mod_n.{h,cc}), key
+// generation (dpf/distributed_point_function.cc:81-222, 642-710).
+// Device side: every evaluation goes through the Tier-1 C ABI
+// (dpf_amd_expand_and_correct / dpf_amd_evaluate_seeds /
+// dpf_amd_evaluate_points / dpf_amd_gather_rows); there is no CPU path.
+#include "dpf_amd/distributed_point_function.h"
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <sstream>
+#include <unordered_map>
+
+#include "host_aes.h"
+#include "internal.h"
+
+namespace distributed_point_functions {
+
+using dpf_amd::HostAes;
+using dpf_amd::u128;
+
+namespace dpf_internal {
+
+// ---------------------------------------------------------------------------
+// Value::Integer <-> uint128 (value_type_helpers.cc:145-166)
+// ---------------------------------------------------------------------------
+Value::Integer Uint128ToValueInteger(uint128 v) {
+  Value::Integer r;
+  if (Uint128High64(v) == 0) {
+    r.set_value_uint64(Uint128Low64(v));
+  } else {
+    r.mutable_value_uint128()->set_high(Uint128High64(v));
+    r.mutable_value_uint128()->set_low(Uint128Low64(v));
+  }
+  return r;
+}
+
+StatusOr<uint128> ValueIntegerToUint128(const Value::Integer& in) {
+  if (in.value_case() == Value::Integer::kValueUint128)
+    return MakeUint128(in.value_uint128().high(), in.value_uint128().low());
+  if (in.value_case() == Value::Integer::kValueUint64) return uint128{in.value_uint64()};
+  return InvalidArgumentError("Unknown value case for the given integer Value");
+}
+
+namespace {
+
+std::string U128ToString(uint128 v) {
+  if (v == 0) return "0";
+  std::string s;
+  while (v) {
+    s.push_back(static_cast<char>('0' + static_cast<int>(v % 10)));
+    v /= 10;
+  }
+  std::reverse(s.begin(), s.end());
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// ValueType validation / equality / BitsNeeded
+// ---------------------------------------------------------------------------
+Status ValidateIntegerType(const ValueType::Integer& t) {
+  int b = t.bitsize();
+  if (b < 1) return InvalidArgumentError("`bitsize` must be positive");
+  if (b > 128) return InvalidArgumentError("`bitsize` must be less than or equal to 128");
+  if ((b & (b - 1)) != 0) return InvalidArgumentError("`bitsize` must be a power of 2");
+  return OkStatus();
+}
+
+Status ValidateIntegerValue(const Value::Integer& v, const ValueType::Integer& t) {
+  if (t.bitsize() < 128) {
+    StatusOr<uint128> x = ValueIntegerToUint128(v);
+    if (!x.ok()) return x.status();
+    if (*x >= (uint128{1} << t.bitsize()))
+      return InvalidArgumentError("Value (= " + U128ToString(*x) +
+                                  ") too large for ValueType with bitsize = " +
+                                  std::to_string(t.bitsize()));
+  }
+  return OkStatus();
+}
+
+Status ValidateValueType(const ValueType& vt) {  // proto_validator.cc:269-287
+  switch (vt.type_case()) {
+    case ValueType::kInteger:
+      return ValidateIntegerType(vt.integer());
+    case ValueType::kTuple:
+      for (const ValueType& e : vt.tuple().elements()) DPF_RETURN_IF_ERROR(ValidateValueType(e));
+      return OkStatus();
+    case ValueType::kIntModN:
+      DPF_RETURN_IF_ERROR(ValidateIntegerType(vt.int_mod_n().base_integer()));
+      return ValidateIntegerValue(vt.int_mod_n().modulus(), vt.int_mod_n().base_integer());
+    case ValueType::kXorWrapper:
+      return ValidateIntegerType(vt.xor_wrapper());
+    default:
+      return InvalidArgumentError("ValidateValueType: Unsupported ValueType:\n" +
+                                  vt.DebugString());
+  }
+}
+
+}  // namespace
+
+StatusOr<bool> ValueTypesAreEqual(const ValueType& lhs, const ValueType& rhs) {
+  if (lhs.type_case() == ValueType::TYPE_NOT_SET || rhs.type_case() == ValueType::TYPE_NOT_SET)
+    return InvalidArgumentError("Both arguments must be valid ValueTypes");
+  if (lhs.type_case() == ValueType::kInteger && rhs.type_case() == ValueType::kInteger)
+    return lhs.integer().bitsize() == rhs.integer().bitsize();
+  if (lhs.type_case() == ValueType::kTuple && rhs.type_case() == ValueType::kTuple &&
+      lhs.tuple().elements_size() == rhs.tuple().elements_size()) {
+    bool result = true;
+    for (int i = 0; i < lhs.tuple().elements_size(); ++i) {
+      StatusOr<bool> e = ValueTypesAreEqual(lhs.tuple().elements(i), rhs.tuple().elements(i));
+      if (!e.ok()) return e.status();
+      result &= *e;
+    }
+    return result;
+  }
+  if (lhs.type_case() == ValueType::kIntModN && rhs.type_case() == ValueType::kIntModN) {
+    StatusOr<uint128> a = ValueIntegerToUint128(lhs.int_mod_n().modulus());
+    if (!a.ok()) return a.status();
+    StatusOr<uint128> b = ValueIntegerToUint128(rhs.int_mod_n().modulus());
+    if (!b.ok()) return b.status();
+    return lhs.int_mod_n().base_integer().bitsize() == rhs.int_mod_n().base_integer().bitsize() &&
+           *a == *b;
+  }
+  if (lhs.type_case() == ValueType::kXorWrapper && rhs.type_case() == ValueType::kXorWrapper)
+    return lhs.xor_wrapper().bitsize() == rhs.xor_wrapper().bitsize();
+  return false;
+}
+
+namespace {
+
+// absl::uint128 -> double (absl/numeric/int128.h).
+double ToDouble(uint128 v) {
+  return static_cast<double>(Uint128Low64(v)) + std::ldexp(static_cast<double>(Uint128High64(v)), 64);
+}
+
+// IntModNBase::CheckParameters + GetNumBytesRequired (int_mod_n.cc:29-84).
+StatusOr<int> IntModNBytesRequired(int num_samples, int base_bits, uint128 modulus,
+                                   double security_parameter) {
+  if (num_samples <= 0) return InvalidArgumentError("num_samples must be positive");
+  if (base_bits <= 0) return InvalidArgumentError("base_integer_bitsize must be positive");
+  if (base_bits > 128) return InvalidArgumentError("base_integer_bitsize must be at most 128");
+  if (base_bits < 128 && (uint128{1} << base_bits) < modulus)
+    return InvalidArgumentError("kModulus " + U128ToString(modulus) +
+                                " out of range for base_integer_bitsize = " +
+                                std::to_string(base_bits));
+  const double sigma = 128 + 3 -
+                       (std::log2(ToDouble(modulus)) + std::log2(static_cast<double>(num_samples)) +
+                        std::log2(static_cast<double>(num_samples + 1)));
+  if (security_parameter > sigma) {
+    char buf[64];
+    snprintf(buf, sizeof(buf), "%f", sigma);
+    return InvalidArgumentError("For num_samples = " + std::to_string(num_samples) +
+                                " and kModulus = " + U128ToString(modulus) +
+                                " this approach can only provide " + buf +
+                                " bits of statistical security. You can try calling this "
+                                "function several times with smaller values of num_samples.");
+  }
+  return 16 + ((base_bits + 7) / 8) * (num_samples - 1);
+}
+
+}  // namespace
+
+// BitsNeeded (value_type_helpers.cc:71-141), including the reference's
+// iteration over elements(i) for i < num_other (lines 105-114).
+StatusOr<int> BitsNeeded(const ValueType& vt, double security_parameter) {
+  switch (vt.type_case()) {
+    case ValueType::kInteger:
+      return vt.integer().bitsize();
+    case ValueType::kTuple: {
+      int num_ints_mod_n = 0, num_other = 0;
+      const ValueType* int_mod_n = nullptr;
+      for (const ValueType& el : vt.tuple().elements()) {
+        if (el.type_case() == ValueType::kIntModN) {
+          if (!int_mod_n) {
+            int_mod_n = &el;
+          } else {
+            StatusOr<bool> eq = ValueTypesAreEqual(el, *int_mod_n);
+            if (!eq.ok()) return eq.status();
+            if (!*eq)
+              return UnimplementedError("All elements of type IntModN in a tuple must be the same");
+          }
+          ++num_ints_mod_n;
+        } else {
+          ++num_other;
+        }
+      }
+      int bitsize_other = 0, bitsize_mod_n = 0;
+      for (int i = 0; i < num_other; ++i) {
+        double per = security_parameter + std::log2(static_cast<double>(num_other));
+        StatusOr<int> b = BitsNeeded(vt.tuple().elements(i), per);
+        if (!b.ok()) return b.status();
+        bitsize_other += *b;
+      }
+      if (num_ints_mod_n > 0) {
+        StatusOr<uint128> m = ValueIntegerToUint128(int_mod_n->int_mod_n().modulus());
+        if (!m.ok()) return m.status();
+        StatusOr<int> bytes = IntModNBytesRequired(
+            num_ints_mod_n, int_mod_n->int_mod_n().base_integer().bitsize(), *m,
+            security_parameter);
+        if (!bytes.ok()) return bytes.status();
+        bitsize_mod_n = *bytes * 8;
+      }
+      return bitsize_mod_n + bitsize_other;
+    }
+    case ValueType::kIntModN: {
+      StatusOr<uint128> m = ValueIntegerToUint128(vt.int_mod_n().modulus());
+      if (!m.ok()) return m.status();
+      StatusOr<int> bytes = IntModNBytesRequired(1, vt.int_mod_n().base_integer().bitsize(), *m,
+                                                 security_parameter);
+      if (!bytes.ok()) return bytes.status();
+      return 8 * *bytes;
+    }
+    case ValueType::kXorWrapper:
+      return vt.xor_wrapper().bitsize();
+    default:
+      return InvalidArgumentError("BitsNeeded: Unsupported ValueType:\n" + vt.DebugString());
+  }
+}
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Flattened value types
+// ---------------------------------------------------------------------------
+struct ScalarMeta {
+  int kind;  // DPF_AMD_KIND_*
+  int bits;
+  uint128 modulus;
+};
+
+struct Node {  // layout computation
+  int size = 0, align = 1;
+};
+
+void Flatten(const ValueType& vt, std::vector<ScalarMeta>* out) {
+  switch (vt.type_case()) {
+    case ValueType::kInteger:
+      out->push_back({DPF_AMD_KIND_INTEGER, vt.integer().bitsize(), 0});
+      break;
+    case ValueType::kXorWrapper:
+      out->push_back({DPF_AMD_KIND_XOR_WRAPPER, vt.xor_wrapper().bitsize(), 0});
+      break;
+    case ValueType::kIntModN: {
+      StatusOr<uint128> m = ValueIntegerToUint128(vt.int_mod_n().modulus());
+      out->push_back({DPF_AMD_KIND_INT_MOD_N, vt.int_mod_n().base_integer().bitsize(),
+                      m.ok() ? *m : 0});
+      break;
+    }
+    case ValueType::kTuple:
+      for (const ValueType& e : vt.tuple().elements()) Flatten(e, out);
+      break;
+    default:
+      break;
+  }
+}
+
+// Host (libstdc++ / Itanium) layout: std::tuple members in reverse order,
+// each at the next suitably aligned offset.  Appends scalar offsets
+// (declaration order) relative to `base`.
+Node Layout(const ValueType& vt, int base, std::vector<int>* offsets) {
+  if (vt.type_case() == ValueType::kTuple) {
+    const int n = vt.tuple().elements_size();
+    std::vector<Node> nodes(n);
+    std::vector<std::vector<int>> sub(n);
+    for (int i = 0; i < n; ++i) nodes[i] = Layout(vt.tuple().elements(i), 0, &sub[i]);
+    std::vector<int> elem_off(n);
+    int end = 0, align = 1;
+    for (int i = n - 1; i >= 0; --i) {
+      int off = (end + nodes[i].align - 1) / nodes[i].align * nodes[i].align;
+      elem_off[i] = off;
+      end = off + nodes[i].size;
+      align = std::max(align, nodes[i].align);
+    }
+    for (int i = 0; i < n; ++i)
+      for (int o : sub[i]) offsets->push_back(base + elem_off[i] + o);
+    Node r;
+    r.align = align;
+    r.size = std::max(1, (end + align - 1) / align * align);
+    return r;
+  }
+  int bits = vt.type_case() == ValueType::kIntModN ? vt.int_mod_n().base_integer().bitsize()
+             : vt.type_case() == ValueType::kXorWrapper ? vt.xor_wrapper().bitsize()
+                                                         : vt.integer().bitsize();
+  Node r;
+  r.size = r.align = std::max(1, bits / 8);
+  offsets->push_back(base);
+  return r;
+}
+
+uint128 MaskBits(int bits) { return bits >= 128 ? ~uint128{0} : ((uint128{1} << bits) - 1); }
+
+uint128 ScAdd(const ScalarMeta& s, uint128 a, uint128 b) {
+  if (s.kind == DPF_AMD_KIND_INTEGER) return (a + b) & MaskBits(s.bits);
+  if (s.kind == DPF_AMD_KIND_XOR_WRAPPER) return a ^ b;
+  uint128 x = s.modulus - b;
+  return a >= x ? a - x : s.modulus - x + a;
+}
+uint128 ScSub(const ScalarMeta& s, uint128 a, uint128 b) {
+  if (s.kind == DPF_AMD_KIND_INTEGER) return (a - b) & MaskBits(s.bits);
+  if (s.kind == DPF_AMD_KIND_XOR_WRAPPER) return a ^ b;
+  return a >= b ? a - b : s.modulus - b + a;
+}
+uint128 ScNeg(const ScalarMeta& s, uint128 a) {
+  if (s.kind == DPF_AMD_KIND_INTEGER) return (uint128{0} - a) & MaskBits(s.bits);
+  if (s.kind == DPF_AMD_KIND_XOR_WRAPPER) return a;
+  return a == 0 ? 0 : s.modulus - a;
+}
+
+uint128 LeBytes(const uint8_t* p, int n) {
+  uint128 v = 0;
+  for (int i = n - 1; i >= 0; --i) v = (v << 8) | p[i];
+  return v;
+}
+
+}  // namespace
+
+// Per hierarchy level metadata.
+struct LevelMeta {
+  std::vector<ScalarMeta> scalars;
+  bool direct = true;
+  int total_bits = 0;
+  int epb = 1;
+  int esz = 0;
+  int bn = 1;
+  int tree_level = 0;
+  int log_domain = 0;
+  dpf_amd_value_type desc{};  // conversion metadata + rule-based host layout
+
+  // ConvertBytesToArrayOf<T> (vth:586-606) on the host (key generation).
+  void Convert(const uint8_t* bytes, int len, std::vector<uint128>* out) const {
+    const int ns = static_cast<int>(scalars.size());
+    out->assign(static_cast<size_t>(epb) * ns, 0);
+    if (direct) {
+      for (int e = 0; e < epb; ++e) {
+        int off = e * esz;
+        for (int s = 0; s < ns; ++s) {
+          int b = scalars[s].bits / 8;
+          (*out)[e * ns + s] = off + b <= len ? LeBytes(bytes + off, b) : 0;
+          off += b;
+        }
+      }
+      return;
+    }
+    uint128 block = LeBytes(bytes, 16);
+    int pos = 16;
+    for (int s = 0; s < ns; ++s) {
+      const ScalarMeta& m = scalars[s];
+      const bool update = s + 1 < ns;
+      const int b = m.bits / 8;
+      if (m.kind == DPF_AMD_KIND_INT_MOD_N) {
+        uint128 q = block / m.modulus, r = block % m.modulus;
+        (*out)[s] = r;
+        if (update) {
+          block = b < 16 ? (q << (8 * b)) : 0;
+          block |= pos + b <= len ? LeBytes(bytes + pos, b) : 0;
+          pos += b;
+        }
+      } else {
+        (*out)[s] = block & MaskBits(m.bits);
+        if (update) {
+          block = b < 16 ? (block & ~MaskBits(m.bits)) : 0;
+          block |= pos + b <= len ? LeBytes(bytes + pos, b) : 0;
+          pos += b;
+        }
+      }
+    }
+  }
+};
+
+class DpfState {
+ public:
+  std::vector<DpfParameters> parameters;
+  int tree_levels_needed = 0;
+  std::vector<int> hierarchy_to_tree;
+  std::vector<int> tree_to_hierarchy;  // -1 if none
+  std::vector<LevelMeta> levels;
+  HostAes prg_left{MakeUint128(dpf_amd::kPrgKeyLeftHi, dpf_amd::kPrgKeyLeftLo)};
+  HostAes prg_right{MakeUint128(dpf_amd::kPrgKeyRightHi, dpf_amd::kPrgKeyRightLo)};
+  HostAes prg_value{MakeUint128(dpf_amd::kPrgKeyValueHi, dpf_amd::kPrgKeyValueLo)};
+};
+
+namespace {
+
+Status ValidateValueOfType(const Value& value, const ValueType& type) {
+  // proto_validator.cc:289-333
+  switch (type.type_case()) {
+    case ValueType::kInteger:
+      if (value.value_case() != Value::kInteger)
+        return InvalidArgumentError("Expected integer value");
+      return ValidateIntegerValue(value.integer(), type.integer());
+    case ValueType::kTuple: {
+      if (value.value_case() != Value::kTuple) return InvalidArgumentError("Expected tuple value");
+      if (value.tuple().elements_size() != type.tuple().elements_size())
+        return InvalidArgumentError("Expected tuple value of size " +
+                                    std::to_string(type.tuple().elements_size()) +
+                                    " but got size " +
+                                    std::to_string(value.tuple().elements_size()));
+      for (int i = 0; i < type.tuple().elements_size(); ++i)
+        DPF_RETURN_IF_ERROR(ValidateValueOfType(value.tuple().elements(i), type.tuple().elements(i)));
+      return OkStatus();
+    }
+    case ValueType::kIntModN: {
+      DPF_RETURN_IF_ERROR(ValidateIntegerValue(value.int_mod_n(), type.int_mod_n().base_integer()));
+      StatusOr<uint128> v = ValueIntegerToUint128(value.int_mod_n());
+      if (!v.ok()) return v.status();
+      StatusOr<uint128> m = ValueIntegerToUint128(type.int_mod_n().modulus());
+      if (!m.ok()) return m.status();
+      if (*v >= *m)
+        return InvalidArgumentError("Value (= " + U128ToString(*v) +
+                                    ") is too large for modulus (= " + U128ToString(*m) + ")");
+      return OkStatus();
+    }
+    case ValueType::kXorWrapper:
+      if (value.value_case() != Value::kXorWrapper)
+        return InvalidArgumentError("Expected XorWrapper value");
+      return ValidateIntegerValue(value.xor_wrapper(), type.xor_wrapper());
+    default:
+      return InvalidArgumentError("ValidateValue: Unsupported ValueType:\n" + type.DebugString());
+  }
+}
+
+// Flattens a (validated) Value of `type`.
+Status FlattenValue(const Value& v, const ValueType& type, std::vector<uint128>* out) {
+  if (type.type_case() == ValueType::kTuple) {
+    if (v.value_case() != Value::kTuple)
+      return InvalidArgumentError("The given Value is not a tuple");
+    if (v.tuple().elements_size() != type.tuple().elements_size())
+      return InvalidArgumentError("The tuple in the given Value has the wrong number of elements");
+    for (int i = 0; i < type.tuple().elements_size(); ++i)
+      DPF_RETURN_IF_ERROR(FlattenValue(v.tuple().elements(i), type.tuple().elements(i), out));
+    return OkStatus();
+  }
+  const Value::Integer* in = nullptr;
+  int bits = 0;
+  switch (type.type_case()) {
+    case ValueType::kInteger:
+      if (v.value_case() != Value::kInteger)
+        return InvalidArgumentError("The given Value is not an integer");
+      in = &v.integer();
+      bits = type.integer().bitsize();
+      break;
+    case ValueType::kIntModN: {
+      if (v.value_case() != Value::kIntModN)
+        return InvalidArgumentError("The given Value is not an IntModN");
+      in = &v.int_mod_n();
+      bits = type.int_mod_n().base_integer().bitsize();
+      break;
+    }
+    case ValueType::kXorWrapper:
+      in = &v.xor_wrapper();
+      bits = type.xor_wrapper().bitsize();
+      break;
+    default:
+      return InvalidArgumentError("unsupported value type");
+  }
+  StatusOr<uint128> x = ValueIntegerToUint128(*in);
+  if (!x.ok()) return x.status();
+  if (bits < 128 && *x > MaskBits(bits))
+    return InvalidArgumentError("Value (= " + std::to_string(static_cast<uint64_t>(*x)) +
+                                ") too large for the given type T (size " +
+                                std::to_string(bits / 8) + ")");
+  if (type.type_case() == ValueType::kIntModN) {
+    StatusOr<uint128> m = ValueIntegerToUint128(type.int_mod_n().modulus());
+    if (m.ok() && *x >= *m)
+      return InvalidArgumentError("The given value (= " + U128ToString(*x) +
+                                  ") is larger than kModulus (= " + U128ToString(*m) + ")");
+  }
+  out->push_back(*x);
+  return OkStatus();
+}
+
+// Builds a Value of `type` from flattened scalars (ToValue<T>).
+Value UnflattenValue(const ValueType& type, const uint128*& it) {
+  Value v;
+  switch (type.type_case()) {
+    case ValueType::kTuple:
+      for (const ValueType& e : type.tuple().elements())
+        *v.mutable_tuple()->add_elements() = UnflattenValue(e, it);
+      break;
+    case ValueType::kIntModN:
+      *v.mutable_int_mod_n() = Uint128ToValueInteger(*it++);
+      break;
+    case ValueType::kXorWrapper:
+      *v.mutable_xor_wrapper() = Uint128ToValueInteger(*it++);
+      break;
+    default:
+      *v.mutable_integer() = Uint128ToValueInteger(*it++);
+      break;
+  }
+  return v;
+}
+
+bool AlmostEqual(double a, double b) { return std::abs(a - b) <= 0.0001; }
+
+double DefaultSecurity(const DpfParameters& p) { return 40 + p.log_domain_size(); }
+
+StatusOr<bool> ParametersAreEqual(const DpfParameters& lhs, const DpfParameters& rhs) {
+  if (lhs.log_domain_size() != rhs.log_domain_size()) return false;
+  if (!(AlmostEqual(lhs.security_parameter(), rhs.security_parameter()) ||
+        (lhs.security_parameter() == 0 &&
+         AlmostEqual(rhs.security_parameter(), DefaultSecurity(rhs))) ||
+        (rhs.security_parameter() == 0 &&
+         AlmostEqual(lhs.security_parameter(), DefaultSecurity(lhs)))))
+    return false;
+  return ValueTypesAreEqual(lhs.value_type(), rhs.value_type());
+}
+
+Status ValidateParameters(Span<const DpfParameters> parameters) {
+  if (parameters.empty()) return InvalidArgumentError("`parameters` must not be empty");
+  int previous = 0;
+  for (size_t i = 0; i < parameters.size(); ++i) {
+    int ld = parameters[i].log_domain_size();
+    if (ld < 0) return InvalidArgumentError("`log_domain_size` must be non-negative");
+    if (ld > 128) return InvalidArgumentError("`log_domain_size` must be <= 128");
+    if (i > 0 && ld <= previous)
+      return InvalidArgumentError(
+          "`log_domain_size` fields must be in ascending order in `parameters`");
+    previous = ld;
+    if (!parameters[i].has_value_type()) return InvalidArgumentError("`value_type` is required");
+    DPF_RETURN_IF_ERROR(ValidateValueType(parameters[i].value_type()));
+    double sp = parameters[i].security_parameter();
+    if (std::isnan(sp)) return InvalidArgumentError("`security_parameter` must not be NaN");
+    if (sp < 0 || sp > 128) return InvalidArgumentError("`security_parameter` must be in [0, 128]");
+  }
+  return OkStatus();
+}
+
+}  // namespace
+
+// Builds the per-level metadata (+ ProtoValidator::Create, proto_validator.cc:113-158).
+StatusOr<std::unique_ptr<DpfState>> MakeDpfState(Span<const DpfParameters> parameters_in) {
+  DPF_RETURN_IF_ERROR(ValidateParameters(parameters_in));
+  auto st = std::make_unique<DpfState>();
+  st->parameters.assign(parameters_in.begin(), parameters_in.end());
+  for (DpfParameters& p : st->parameters)
+    if (p.security_parameter() == 0) p.set_security_parameter(DefaultSecurity(p));
+  const int n = static_cast<int>(st->parameters.size());
+  st->hierarchy_to_tree.resize(n);
+  st->tree_to_hierarchy.assign(130, -1);
+  st->levels.resize(n);
+  int tree_levels_needed = 0;
+  for (int i = 0; i < n; ++i) {
+    const DpfParameters& p = st->parameters[i];
+    StatusOr<int> bits = BitsNeeded(p.value_type(), p.security_parameter());
+    if (!bits.ok()) return bits.status();
+    int log_bits_needed = static_cast<int>(std::ceil(std::log2(*bits)));
+    int tree_level = std::max(tree_levels_needed,
+                              p.log_domain_size() - 7 + std::min(log_bits_needed, 7));
+    st->tree_to_hierarchy[tree_level] = i;
+    st->hierarchy_to_tree[i] = tree_level;
+    tree_levels_needed = std::max(tree_levels_needed, tree_level + 1);
+
+    LevelMeta& m = st->levels[i];
+    Flatten(p.value_type(), &m.scalars);
+    m.total_bits = 0;
+    m.direct = true;
+    for (const ScalarMeta& s : m.scalars) {
+      m.total_bits += s.bits;
+      if (s.kind == DPF_AMD_KIND_INT_MOD_N) m.direct = false;
+    }
+    m.epb = (m.direct && m.total_bits <= 128 && m.total_bits > 0) ? 128 / m.total_bits : 1;
+    m.esz = (m.total_bits + 7) / 8;
+    m.bn = (*bits + 127) / 128;
+    m.tree_level = tree_level;
+    m.log_domain = p.log_domain_size();
+    dpf_amd_value_type& d = m.desc;
+    memset(&d, 0, sizeof(d));
+    d.num_scalars = static_cast<int32_t>(m.scalars.size());
+    d.directly_convertible = m.direct ? 1 : 0;
+    d.elements_per_block = m.epb;
+    d.element_size = m.esz;
+    d.blocks_needed = m.bn;
+    std::vector<int> offs;
+    Node node = Layout(p.value_type(), 0, &offs);
+    d.out_stride = node.size;
+    int in_off = 0;
+    for (size_t s = 0; s < m.scalars.size() && s < DPF_AMD_MAX_SCALARS; ++s) {
+      d.scalars[s].kind = m.scalars[s].kind;
+      d.scalars[s].bytes = m.scalars[s].bits / 8;
+      d.scalars[s].in_offset = in_off;
+      d.scalars[s].out_offset = offs[s];
+      d.scalars[s].modulus[0] = Uint128Low64(m.scalars[s].modulus);
+      d.scalars[s].modulus[1] = Uint128High64(m.scalars[s].modulus);
+      in_off += m.scalars[s].bits / 8;
+    }
+  }
+  st->tree_levels_needed = tree_levels_needed;
+  return st;
+}
+
+}  // namespace dpf_internal
+
+using dpf_internal::DpfState;
+using dpf_internal::LevelMeta;
+
+std::string ValueType::DebugString() const {
+  std::ostringstream os;
+  switch (case_) {
+    case kInteger:
+      os << "integer { bitsize: " << integer_.bitsize() << " }\n";
+      break;
+    case kXorWrapper:
+      os << "xor_wrapper { bitsize: " << integer_.bitsize() << " }\n";
+      break;
+    case kIntModN:
+      os << "int_mod_n { base_integer { bitsize: " << int_mod_n_.base_integer().bitsize()
+         << " } }\n";
+      break;
+    case kTuple:
+      os << "tuple {\n";
+      for (const ValueType& e : tuple_.elements()) os << "  elements { " << e.DebugString() << "}\n";
+      os << "}\n";
+      break;
+    default:
+      break;
+  }
+  return os.str();
+}
+
+std::string DpfParameters::DebugString() const {
+  std::ostringstream os;
+  os << "log_domain_size: " << log_domain_size_ << "\nvalue_type {\n"
+     << value_type_.DebugString() << "}\nsecurity_parameter: " << security_parameter_ << "\n";
+  return os.str();
+}
+
+// ---------------------------------------------------------------------------
+// Device helpers
+// ---------------------------------------------------------------------------
+namespace {
+
+Status HipStatus(hipError_t e, const char* what) {
+  if (e == hipSuccess) return OkStatus();
+  if (e == hipErrorOutOfMemory)
+    return ResourceExhaustedError(std::string(what) + ": " + hipGetErrorString(e));
+  return InternalError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+Status AbiStatus(int rc) {
+  if (rc == DPF_AMD_OK) return OkStatus();
+  return Status(static_cast<StatusCode>(rc), dpf_amd::LastError());
+}
+
+hipStream_t ThreadStream() {
+  thread_local hipStream_t s = [] {
+    hipStream_t x = nullptr;
+    if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) x = nullptr;
+    return x;
+  }();
+  return s;
+}
+
+class DeviceBuffer {
+ public:
+  DeviceBuffer() = default;
+  ~DeviceBuffer() { Reset(); }
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+  Status Alloc(size_t bytes, hipStream_t s) {
+    Reset();
+    stream_ = s;
+    if (bytes == 0) bytes = 16;
+    return HipStatus(hipMallocAsync(&p_, bytes, s), "hipMallocAsync");
+  }
+  Status Upload(const void* src, size_t bytes, hipStream_t s) {
+    DPF_RETURN_IF_ERROR(Alloc(bytes, s));
+    if (bytes == 0) return OkStatus();
+    return HipStatus(hipMemcpyAsync(p_, src, bytes, hipMemcpyHostToDevice, s), "upload");
+  }
+  void Reset() {
+    if (p_) hipFreeAsync(p_, stream_);
+    p_ = nullptr;
+  }
+  void* get() const { return p_; }
+  template <typename T>
+  T* as() const {
+    return static_cast<T*>(p_);
+  }
+
+ private:
+  void* p_ = nullptr;
+  hipStream_t stream_ = nullptr;
+};
+
+struct CwArrays {
+  std::vector<uint128> seeds;
+  std::vector<uint8_t> ccl, ccr;
+};
+
+CwArrays KeyCws(const DpfKey& key, int start, int stop) {
+  CwArrays c;
+  for (int i = start; i < stop; ++i) {
+    const CorrectionWord& cw = key.correction_words(i);
+    c.seeds.push_back(MakeUint128(cw.seed().high(), cw.seed().low()));
+    c.ccl.push_back(cw.control_left() ? 1 : 0);
+    c.ccr.push_back(cw.control_right() ? 1 : 0);
+  }
+  return c;
+}
+
+struct U128Hash {
+  size_t operator()(const uint128& v) const {
+    uint64_t h = static_cast<uint64_t>(v) * 0x9E3779B97F4A7C15ull ^
+                 (static_cast<uint64_t>(v >> 64) + 0x632BE59BD9B4E019ull);
+    h ^= h >> 29;
+    return static_cast<size_t>(h * 0xBF58476D1CE4E5B9ull);
+  }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// DistributedPointFunction
+// ---------------------------------------------------------------------------
+
+DistributedPointFunction::DistributedPointFunction(std::unique_ptr<DpfState> s)
+    : state_(std::move(s)) {}
+DistributedPointFunction::~DistributedPointFunction() = default;
+
+StatusOr<std::unique_ptr<DistributedPointFunction>> DistributedPointFunction::Create(
+    const DpfParameters& parameters) {
+  return CreateIncremental(Span<const DpfParameters>(&parameters, 1));
+}
+
+StatusOr<std::unique_ptr<DistributedPointFunction>> DistributedPointFunction::CreateIncremental(
+    Span<const DpfParameters> parameters) {
+  StatusOr<std::unique_ptr<DpfState>> st = dpf_internal::MakeDpfState(parameters);
+  if (!st.ok()) return st.status();
+  return std::unique_ptr<DistributedPointFunction>(
+      new DistributedPointFunction(std::move(*st)));
+}
+
+Span<const DpfParameters> DistributedPointFunction::parameters() const {
+  return Span<const DpfParameters>(state_->parameters.data(), state_->parameters.size());
+}
+int DistributedPointFunction::num_hierarchy_levels() const {
+  return static_cast<int>(state_->parameters.size());
+}
+int DistributedPointFunction::tree_levels_needed() const { return state_->tree_levels_needed; }
+int DistributedPointFunction::hierarchy_to_tree(int h) const {
+  return state_->hierarchy_to_tree[h];
+}
+int DistributedPointFunction::blocks_needed(int h) const { return state_->levels[h].bn; }
+dpf_amd_value_type DistributedPointFunction::value_type_descriptor(int h) const {
+  return state_->levels[h].desc;
+}
+
+Status DistributedPointFunction::CheckType(const ValueType& type, int level, bool at) const {
+  const int n = num_hierarchy_levels();
+  int lo = level, hi = level + 1;
+  if (level < 0) {
+    lo = 0;
+    hi = n;
+  } else if (level >= n) {
+    return OkStatus();  // range errors are reported by the Raw entry points
+  }
+  for (int h = lo; h < hi; ++h) {
+    StatusOr<bool> eq = dpf_internal::ValueTypesAreEqual(type, state_->parameters[h].value_type());
+    if (!eq.ok()) return eq.status();
+    if (!*eq) {
+      if (at && level >= 0)
+        return InvalidArgumentError("Value type T doesn't match parameters at `hierarchy_level`");
+      return InvalidArgumentError("Value type T doesn't match parameters at `hierarchy_level`");
+    }
+  }
+  return OkStatus();
+}
+
+// --- key generation (cc:81-222, 642-710) -----------------------------------
+
+namespace {
+
+// ComputeValueCorrection (cc:81-117) + ComputeValueCorrectionFor<T> (vth:614-648).
+std::vector<uint128> ComputeValueCorrection(const DpfState& st, int h, const uint128 seeds[2],
+                                            uint128 alpha_prefix,
+                                            const std::vector<uint128>& beta, bool invert) {
+  const LevelMeta& m = st.levels[h];
+  const int bn = m.bn;
+  std::vector<uint128> exp(2 * bn);
+  for (int j = 0; j < bn; ++j) {
+    exp[j] = seeds[0] + static_cast<uint128>(j);
+    exp[bn + j] = seeds[1] + static_cast<uint128>(j);
+  }
+  st.prg_value.MmoHash(exp.data(), exp.data(), exp.size());
+  const int bits = m.log_domain - m.tree_level;
+  const int block_index = static_cast<int>(alpha_prefix & ((uint128{1} << bits) - 1));
+  std::vector<uint128> a, b;
+  m.Convert(reinterpret_cast<const uint8_t*>(exp.data()), 16 * bn, &a);
+  m.Convert(reinterpret_cast<const uint8_t*>(exp.data() + bn), 16 * bn, &b);
+  const int ns = static_cast<int>(m.scalars.size());
+  for (int s = 0; s < ns; ++s)
+    b[block_index * ns + s] = dpf_internal::ScAdd(m.scalars[s], b[block_index * ns + s], beta[s]);
+  for (int e = 0; e < m.epb; ++e)
+    for (int s = 0; s < ns; ++s) {
+      uint128 v = dpf_internal::ScSub(m.scalars[s], b[e * ns + s], a[e * ns + s]);
+      if (invert) v = dpf_internal::ScNeg(m.scalars[s], v);
+      b[e * ns + s] = v;
+    }
+  return b;
+}
+
+void AddCorrectionValues(const DpfState& st, int h, const std::vector<uint128>& vc,
+                         std::vector<Value>* out) {
+  const LevelMeta& m = st.levels[h];
+  const int ns = static_cast<int>(m.scalars.size());
+  for (int e = 0; e < m.epb; ++e) {
+    const uint128* it = vc.data() + e * ns;
+    out->push_back(dpf_internal::UnflattenValue(st.parameters[h].value_type(), it));
+  }
+}
+
+inline bool ExtractAndClearLowestBit(uint128& x) {
+  bool bit = (x & 1) != 0;
+  x &= ~uint128{1};
+  return bit;
+}
+
+}  // namespace
+
+StatusOr<std::pair<DpfKey, DpfKey>> DistributedPointFunction::GenerateKeysIncremental(
+    uint128 alpha, const std::vector<uint128>& beta) {
+  std::vector<Value> values;
+  for (uint128 b : beta) {
+    Value v;
+    *v.mutable_integer() = dpf_internal::Uint128ToValueInteger(b);
+    values.push_back(v);
+  }
+  return GenerateKeysIncremental(alpha, Span<const Value>(values.data(), values.size()));
+}
+
+StatusOr<std::pair<DpfKey, DpfKey>> DistributedPointFunction::GenerateKeysIncremental(
+    uint128 alpha, Span<const Value> beta) {
+  uint128 seeds[2];
+  if (!dpf_amd::SecureRandom(seeds, sizeof(seeds)))
+    return InternalError("Failed to obtain random bytes");
+  return GenerateKeysIncrementalWithSeeds(alpha, beta, seeds[0], seeds[1]);
+}
+
+StatusOr<std::pair<DpfKey, DpfKey>> DistributedPointFunction::GenerateKeysIncrementalWithSeeds(
+    uint128 alpha, Span<const Value> beta, uint128 seed0, uint128 seed1) {
+  const DpfState& st = *state_;
+  const int L = num_hierarchy_levels();
+  if (static_cast<int>(beta.size()) != L)
+    return InvalidArgumentError(
+        "`beta` has to have the same size as `parameters` passed at construction");
+  std::vector<std::vector<uint128>> flat(L);
+  for (int i = 0; i < L; ++i) {
+    DPF_RETURN_IF_ERROR(dpf_internal::ValidateValueOfType(beta[i], st.parameters[i].value_type()));
+    DPF_RETURN_IF_ERROR(dpf_internal::FlattenValue(beta[i], st.parameters[i].value_type(), &flat[i]));
+  }
+  const int last_ld = st.parameters.back().log_domain_size();
+  if (last_ld < 128 && alpha >= (uint128{1} << last_ld))
+    return InvalidArgumentError("`alpha` must be smaller than the output domain size");
+
+  std::array<DpfKey, 2> keys;
+  keys[0].set_party(0);
+  keys[1].set_party(1);
+  uint128 seeds[2] = {seed0, seed1};
+  for (int p = 0; p < 2; ++p) {
+    keys[p].mutable_seed()->set_high(Uint128High64(seeds[p]));
+    keys[p].mutable_seed()->set_low(Uint128Low64(seeds[p]));
+  }
+  bool control_bits[2] = {false, true};
+  for (int i = 1; i < st.tree_levels_needed; ++i) {  // GenerateNext (cc:121-222)
+    CorrectionWord cw;
+    const int h_prev = st.tree_to_hierarchy[i - 1];
+    if (h_prev >= 0) {
+      uint128 alpha_prefix = 0;
+      const int shift = last_ld - st.parameters[h_prev].log_domain_size();
+      if (shift < 128) alpha_prefix = alpha >> shift;
+      std::vector<uint128> vc =
+          ComputeValueCorrection(st, h_prev, seeds, alpha_prefix, flat[h_prev], control_bits[1]);
+      AddCorrectionValues(st, h_prev, vc, cw.mutable_value_correction());
+    }
+    uint128 e[2][2];
+    st.prg_left.MmoHash(seeds, e[0], 2);
+    st.prg_right.MmoHash(seeds, e[1], 2);
+    bool ecb[2][2];
+    for (int b = 0; b < 2; ++b)
+      for (int p = 0; p < 2; ++p) ecb[b][p] = ExtractAndClearLowestBit(e[b][p]);
+    bool current_bit = false;
+    if (last_ld - i < 128) current_bit = ((alpha >> (last_ld - i)) & 1) != 0;
+    const int keep = current_bit ? 1 : 0, lose = 1 - keep;
+    const uint128 seed_correction = e[lose][0] ^ e[lose][1];
+    bool cc[2];
+    cc[0] = ecb[0][0] ^ ecb[0][1] ^ current_bit ^ 1;
+    cc[1] = ecb[1][0] ^ ecb[1][1] ^ current_bit;
+    for (int p = 0; p < 2; ++p) {
+      seeds[p] = e[keep][p];
+      if (control_bits[p]) seeds[p] ^= seed_correction;
+    }
+    for (int p = 0; p < 2; ++p) control_bits[p] = ecb[keep][p] ^ (control_bits[p] && cc[keep]);
+    cw.mutable_seed()->set_high(Uint128High64(seed_correction));
+    cw.mutable_seed()->set_low(Uint128Low64(seed_correction));
+    cw.set_control_left(cc[0]);
+    cw.set_control_right(cc[1]);
+    *keys[0].add_correction_words() = cw;
+    *keys[1].add_correction_words() = cw;
+  }
+  std::vector<uint128> vc =
+      ComputeValueCorrection(st, L - 1, seeds, alpha, flat[L - 1], control_bits[1]);
+  std::vector<Value> last;
+  AddCorrectionValues(st, L - 1, vc, &last);
+  for (int p = 0; p < 2; ++p) *keys[p].mutable_last_level_value_correction() = last;
+  return std::make_pair(std::move(keys[0]), std::move(keys[1]));
+}
+
+// --- validation of keys and contexts (proto_validator.cc:205-267) ----------
+
+namespace {
+
+Status ValidateDpfKey(const DpfState& st, const DpfKey& key) {
+  if (!key.has_seed()) return InvalidArgumentError("key.seed must be present");
+  if (key.last_level_value_correction().empty())
+    return InvalidArgumentError("key.last_level_value_correction must be present");
+  if (key.correction_words_size() != st.tree_levels_needed - 1)
+    return InvalidArgumentError("Malformed DpfKey: expected " +
+                                std::to_string(st.tree_levels_needed - 1) +
+                                " correction words, but got " +
+                                std::to_string(key.correction_words_size()));
+  for (size_t i = 0; i < st.hierarchy_to_tree.size(); ++i) {
+    const int t = st.hierarchy_to_tree[i];
+    if (t == st.tree_levels_needed - 1) continue;
+    if (key.correction_words(t).value_correction().empty())
+      return InvalidArgumentError("Malformed DpfKey: expected correction_words[" +
+                                  std::to_string(t) +
+                                  "] to contain the value correction of hierarchy level " +
+                                  std::to_string(i));
+  }
+  return OkStatus();
+}
+
+Status ValidateEvaluationContext(const DpfState& st, const EvaluationContext& ctx) {
+  if (ctx.parameters_size() != static_cast<int>(st.parameters.size()))
+    return InvalidArgumentError("Number of parameters in `ctx` doesn't match");
+  for (int i = 0; i < ctx.parameters_size(); ++i) {
+    StatusOr<bool> eq = dpf_internal::ParametersAreEqual(st.parameters[i], ctx.parameters(i));
+    if (!eq.ok()) return eq.status();
+    if (!*eq) return InvalidArgumentError("Parameter " + std::to_string(i) + " in `ctx` doesn't match");
+  }
+  if (!ctx.has_key()) return InvalidArgumentError("ctx.key must be present");
+  DPF_RETURN_IF_ERROR(ValidateDpfKey(st, ctx.key()));
+  if (ctx.previous_hierarchy_level() >= ctx.parameters_size() - 1)
+    return InvalidArgumentError("This context has already been fully evaluated");
+  if (!ctx.partial_evaluations().empty() &&
+      ctx.partial_evaluations_level() > ctx.previous_hierarchy_level())
+    return InvalidArgumentError(
+        "ctx.partial_evaluations_level must be less than or equal to "
+        "ctx.previous_hierarchy_level");
+  return OkStatus();
+}
+
+// ValuesToArray<T> (vth:561-580) flattened.
+Status CorrectionsFor(const DpfState& st, const DpfKey& key, int h, std::vector<uint128>* out) {
+  const std::vector<Value>* vals;
+  if (h < static_cast<int>(st.parameters.size()) - 1)
+    vals = &key.correction_words(st.hierarchy_to_tree[h]).value_correction();
+  else
+    vals = &key.last_level_value_correction();
+  const LevelMeta& m = st.levels[h];
+  if (static_cast<int>(vals->size()) != m.epb)
+    return InvalidArgumentError("values.size() (= " + std::to_string(vals->size()) +
+                                ") does not match ElementsPerBlock<T>() (= " +
+                                std::to_string(m.epb) + ")");
+  out->clear();
+  for (const Value& v : *vals)
+    DPF_RETURN_IF_ERROR(dpf_internal::FlattenValue(v, st.parameters[h].value_type(), out));
+  return OkStatus();
+}
+
+// Merges the conversion metadata of level h with the caller's host layout.
+Status MergeLayout(const LevelMeta& m, const dpf_amd_value_type& layout, dpf_amd_value_type* out) {
+  *out = m.desc;
+  if (layout.num_scalars != m.desc.num_scalars)
+    return InvalidArgumentError("Value type T doesn't match parameters at `hierarchy_level`");
+  if (m.desc.num_scalars > DPF_AMD_MAX_SCALARS)
+    return UnimplementedError("too many tuple elements");
+  for (int s = 0; s < m.desc.num_scalars; ++s) {
+    if (m.scalars[s].bits < 8)
+      return UnimplementedError("element bit sizes below 8 are not supported");
+    out->scalars[s].out_offset = layout.scalars[s].out_offset;
+  }
+  out->out_stride = layout.out_stride;
+  return OkStatus();
+}
+
+}  // namespace
+
+StatusOr<EvaluationContext> DistributedPointFunction::CreateEvaluationContext(DpfKey key) const {
+  DPF_RETURN_IF_ERROR(ValidateDpfKey(*state_, key));
+  EvaluationContext r;
+  for (const DpfParameters& p : state_->parameters) *r.add_parameters() = p;
+  *r.mutable_key() = std::move(key);
+  r.set_previous_hierarchy_level(-1);
+  return r;
+}
+
+// --- evaluation --------------------------------------------------------------
+
+namespace {
+
+// ComputePartialEvaluations (cc:374-476): selects the stored partial
+// evaluations for `prefixes` (host map, as the reference's btree), walks them
+// on the device to `hierarchy_level`'s tree level, and rewrites ctx.
+// Returns device seeds / control bits for the prefixes.
+Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixes,
+                                 int hierarchy_level, bool update_ctx, EvaluationContext& ctx,
+                                 hipStream_t s, DeviceBuffer* seeds_dev, DeviceBuffer* cb_dev) {
+  const int64_t n = static_cast<int64_t>(prefixes.size());
+  int start_level = st.hierarchy_to_tree[ctx.partial_evaluations_level()];
+  const int stop_level = st.hierarchy_to_tree[hierarchy_level];
+  std::vector<uint128> seeds(n);
+  std::vector<uint8_t> cbs(n);
+  if (ctx.partial_evaluations_size() > 0 && start_level <= stop_level) {
+    std::unordered_map<uint128, std::pair<uint128, bool>, U128Hash> prev;
+    prev.reserve(ctx.partial_evaluations_size() * 2);
+    for (const PartialEvaluation& e : ctx.partial_evaluations()) {
+      const uint128 prefix = MakeUint128(e.prefix().high(), e.prefix().low());
+      const std::pair<uint128, bool> value{MakeUint128(e.seed().high(), e.seed().low()),
+                                           e.control_bit()};
+      auto it = prev.emplace(prefix, value).first;
+      if (it->second != value)
+        return InvalidArgumentError(
+            "Duplicate prefix in `ctx.partial_evaluations()` with mismatching seed or "
+            "control bit");
+    }
+    const int shift = stop_level - start_level;
+    for (int64_t i = 0; i < n; ++i) {
+      const uint128 pp = shift < 128 ? (prefixes[i] >> shift) : 0;
+      auto it = prev.find(pp);
+      if (it == prev.end())
+        return InvalidArgumentError(
+            "Prefix not present in ctx.partial_evaluations at hierarchy level " +
+            std::to_string(hierarchy_level));
+      seeds[i] = it->second.first;
+      cbs[i] = it->second.second ? 1 : 0;
+    }
+  } else {
+    const uint128 seed = MakeUint128(ctx.key().seed().high(), ctx.key().seed().low());
+    std::fill(seeds.begin(), seeds.end(), seed);
+    std::fill(cbs.begin(), cbs.end(), static_cast<uint8_t>(ctx.key().party() != 0));
+    start_level = 0;
+  }
+  const int levels = stop_level - start_level;
+  CwArrays cw = KeyCws(ctx.key(), start_level, stop_level);
+  DeviceBuffer paths, cws, ccl, ccr;
+  DPF_RETURN_IF_ERROR(seeds_dev->Upload(seeds.data(), 16 * n, s));
+  DPF_RETURN_IF_ERROR(cb_dev->Upload(cbs.data(), n, s));
+  if (levels > 0 && n > 0) {
+    DPF_RETURN_IF_ERROR(paths.Upload(prefixes.data(), 16 * n, s));
+    DPF_RETURN_IF_ERROR(cws.Upload(cw.seeds.data(), 16 * levels, s));
+    DPF_RETURN_IF_ERROR(ccl.Upload(cw.ccl.data(), levels, s));
+    DPF_RETURN_IF_ERROR(ccr.Upload(cw.ccr.data(), levels, s));
+    DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_seeds(
+        n, levels, levels, seeds_dev->get(), cb_dev->as<uint8_t>(), paths.get(), 0, cws.get(),
+        ccl.as<uint8_t>(), ccr.as<uint8_t>(), dpf_amd::kPrgKeyLeftLo, dpf_amd::kPrgKeyLeftHi,
+        dpf_amd::kPrgKeyRightLo, dpf_amd::kPrgKeyRightHi, seeds_dev->get(),
+        cb_dev->as<uint8_t>(), s)));
+  }
+  ctx.clear_partial_evaluations();
+  if (update_ctx && n > 0) {
+    DPF_RETURN_IF_ERROR(HipStatus(
+        hipMemcpyAsync(seeds.data(), seeds_dev->get(), 16 * n, hipMemcpyDeviceToHost, s), "d2h"));
+    DPF_RETURN_IF_ERROR(HipStatus(
+        hipMemcpyAsync(cbs.data(), cb_dev->get(), n, hipMemcpyDeviceToHost, s), "d2h"));
+    DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+    std::vector<PartialEvaluation>* pe = ctx.mutable_partial_evaluations();
+    pe->resize(n);
+    for (int64_t i = 0; i < n; ++i) {
+      PartialEvaluation& e = (*pe)[i];
+      e.mutable_prefix()->set_high(Uint128High64(prefixes[i]));
+      e.mutable_prefix()->set_low(Uint128Low64(prefixes[i]));
+      e.mutable_seed()->set_high(Uint128High64(seeds[i]));
+      e.mutable_seed()->set_low(Uint128Low64(seeds[i]));
+      e.set_control_bit(cbs[i] != 0);
+    }
+  }
+  ctx.set_partial_evaluations_level(hierarchy_level);
+  return OkStatus();
+}
+
+}  // namespace
+
+Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
+                                                  Span<const uint128> prefixes,
+                                                  EvaluationContext& ctx,
+                                                  const dpf_amd_value_type& layout, void* out,
+                                                  int64_t out_capacity, int64_t* num_outputs,
+                                                  bool out_on_device, void* stream) const {
+  const DpfState& st = *state_;
+  DPF_RETURN_IF_ERROR(ValidateEvaluationContext(st, ctx));
+  const int L = num_hierarchy_levels();
+  if (hierarchy_level < 0 || hierarchy_level >= L)
+    return InvalidArgumentError(
+        "`hierarchy_level` must be non-negative and less than parameters_.size()");
+  if (hierarchy_level <= ctx.previous_hierarchy_level())
+    return InvalidArgumentError(
+        "`hierarchy_level` must be greater than `ctx.previous_hierarchy_level`");
+  if ((ctx.previous_hierarchy_level() < 0) != prefixes.empty())
+    return InvalidArgumentError(
+        "`prefixes` must be empty if and only if this is the first call with `ctx`.");
+  int previous_log_domain_size = 0;
+  const int prev_h = ctx.previous_hierarchy_level();
+  if (!prefixes.empty()) {
+    previous_log_domain_size = st.parameters[prev_h].log_domain_size();
+    for (uint128 p : prefixes)
+      if (previous_log_domain_size < 128 && p >= (uint128{1} << previous_log_domain_size))
+        return InvalidArgumentError("Index " + dpf_internal::U128ToString(p) +
+                                    " out of range for hierarchy level " + std::to_string(prev_h));
+  }
+  const int log_domain_size = st.parameters[hierarchy_level].log_domain_size();
+  if (log_domain_size - previous_log_domain_size > 62)
+    return InvalidArgumentError(
+        "Output size would be larger than 2**62. Please evaluate fewer hierarchy levels at "
+        "once.");
+  const int64_t num_prefixes = static_cast<int64_t>(prefixes.size());
+  const int64_t outputs_per_prefix = int64_t{1} << (log_domain_size - previous_log_domain_size);
+  const int64_t total = prefixes.empty() ? outputs_per_prefix : num_prefixes * outputs_per_prefix;
+  *num_outputs = total;
+  if (out == nullptr) return OkStatus();
+  if (out_capacity < total) return InvalidArgumentError("output buffer too small");
+
+  const LevelMeta& m = st.levels[hierarchy_level];
+  dpf_amd_value_type vt;
+  DPF_RETURN_IF_ERROR(MergeLayout(m, layout, &vt));
+  std::vector<uint128> corr;
+  DPF_RETURN_IF_ERROR(CorrectionsFor(st, ctx.key(), hierarchy_level, &corr));
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ThreadStream();
+
+  // Unique tree indices in first-appearance order (h:772-796).
+  std::vector<uint128> tree_indices;
+  std::vector<std::pair<int64_t, int>> prefix_map;
+  if (!prefixes.empty()) {
+    const int bbits = st.parameters[prev_h].log_domain_size() - st.hierarchy_to_tree[prev_h];
+    std::unordered_map<uint128, int64_t, U128Hash> inverse;
+    inverse.reserve(num_prefixes * 2);
+    tree_indices.reserve(num_prefixes);
+    prefix_map.reserve(num_prefixes);
+    for (int64_t i = 0; i < num_prefixes; ++i) {
+      const uint128 ti = prefixes[i] >> bbits;
+      const int bi = static_cast<int>(prefixes[i] & ((uint128{1} << bbits) - 1));
+      auto it = inverse.emplace(ti, static_cast<int64_t>(tree_indices.size()));
+      if (it.second) tree_indices.push_back(ti);
+      prefix_map.emplace_back(it.first->second, bi);
+    }
+  }
+
+  // ExpandAndUpdateContext (cc:478-521): roots on the device.
+  DeviceBuffer root_seeds, root_cb;
+  int start_level = 0;
+  if (prefixes.empty()) {
+    const uint128 seed = MakeUint128(ctx.key().seed().high(), ctx.key().seed().low());
+    const uint8_t cb = static_cast<uint8_t>(ctx.key().party() != 0);
+    DPF_RETURN_IF_ERROR(root_seeds.Upload(&seed, 16, s));
+    DPF_RETURN_IF_ERROR(root_cb.Upload(&cb, 1, s));
+  } else {
+    const bool update_ctx = hierarchy_level < L - 1;
+    DPF_RETURN_IF_ERROR(ComputePartialEvaluations(
+        st, Span<const uint128>(tree_indices.data(), tree_indices.size()), prev_h, update_ctx,
+        ctx, s, &root_seeds, &root_cb));
+    start_level = st.hierarchy_to_tree[prev_h];
+  }
+  const int stop_level = st.hierarchy_to_tree[hierarchy_level];
+  const int levels = stop_level - start_level;
+  CwArrays cw = KeyCws(ctx.key(), start_level, stop_level);
+  DeviceBuffer cws, ccl, ccr;
+  DPF_RETURN_IF_ERROR(cws.Upload(cw.seeds.data(), 16 * levels, s));
+  DPF_RETURN_IF_ERROR(ccl.Upload(cw.ccl.data(), levels, s));
+  DPF_RETURN_IF_ERROR(ccr.Upload(cw.ccr.data(), levels, s));
+  const int64_t num_roots = prefixes.empty() ? 1 : static_cast<int64_t>(tree_indices.size());
+  const int cepb = 1 << (log_domain_size - stop_level);
+  const int64_t expanded = (num_roots << levels) * cepb;
+  const size_t stride = static_cast<size_t>(vt.out_stride);
+
+  DeviceBuffer staging, result;
+  void* expand_out = nullptr;
+  if (prefixes.empty() && out_on_device) {
+    expand_out = out;
+  } else {
+    DPF_RETURN_IF_ERROR(staging.Alloc(expanded * stride, s));
+    expand_out = staging.get();
+  }
+  DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_expand_and_correct(
+      num_roots, root_seeds.get(), root_cb.as<uint8_t>(), levels, cws.get(), ccl.as<uint8_t>(),
+      ccr.as<uint8_t>(), &vt, reinterpret_cast<const uint64_t*>(corr.data()),
+      ctx.key().party(), cepb, 0, num_roots << levels, expand_out, s)));
+
+  void* final_dev = expand_out;
+  if (!prefixes.empty()) {
+    // Per-prefix slices (h:877-889).
+    const int64_t blocks_per_tree_prefix = int64_t{1} << levels;
+    std::vector<int64_t> src(num_prefixes);
+    for (int64_t i = 0; i < num_prefixes; ++i)
+      src[i] = prefix_map[i].first * blocks_per_tree_prefix * cepb +
+               prefix_map[i].second * outputs_per_prefix;
+    DeviceBuffer src_dev;
+    DPF_RETURN_IF_ERROR(src_dev.Upload(src.data(), 8 * num_prefixes, s));
+    if (out_on_device) {
+      final_dev = out;
+    } else {
+      DPF_RETURN_IF_ERROR(result.Alloc(total * stride, s));
+      final_dev = result.get();
+    }
+    DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_gather_rows(num_prefixes, src_dev.as<int64_t>(),
+                                                      outputs_per_prefix, stride, expand_out,
+                                                      final_dev, s)));
+  }
+  if (!out_on_device)
+    DPF_RETURN_IF_ERROR(HipStatus(
+        hipMemcpyAsync(out, final_dev, total * stride, hipMemcpyDeviceToHost, s), "d2h"));
+  DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+  ctx.set_previous_hierarchy_level(hierarchy_level);
+  return OkStatus();
+}
+
+Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_level,
+                                               Span<const uint128> evaluation_points,
+                                               EvaluationContext* ctx,
+                                               const dpf_amd_value_type& layout,
+                                               void* out) const {
+  const DpfState& st = *state_;
+  if (ctx != nullptr && &key != &ctx->key())
+    return InvalidArgumentError("`key` and `ctx->key()` must refer to the same object");
+  if (hierarchy_level < 0) return InvalidArgumentError("`hierarchy_level` must be non-negative");
+  if (hierarchy_level >= num_hierarchy_levels())
+    return InvalidArgumentError(
+        "`hierarchy_level` must be less than the number of parameters passed at construction");
+  const int64_t n = static_cast<int64_t>(evaluation_points.size());
+  const int log_domain_size = st.parameters[hierarchy_level].log_domain_size();
+  uint128 max_point = Uint128Max();
+  if (log_domain_size < 128) max_point = (uint128{1} << log_domain_size) - 1;
+  for (int64_t i = 0; i < n; ++i)
+    if (evaluation_points[i] > max_point)
+      return InvalidArgumentError("`evaluation_points[" + std::to_string(i) +
+                                  "]` larger than the domain size at hierarchy level " +
+                                  std::to_string(hierarchy_level));
+  DPF_RETURN_IF_ERROR(ValidateDpfKey(st, key));
+  if (n == 0) return OkStatus();
+  const LevelMeta& m = st.levels[hierarchy_level];
+  dpf_amd_value_type vt;
+  DPF_RETURN_IF_ERROR(MergeLayout(m, layout, &vt));
+  std::vector<uint128> corr;
+  DPF_RETURN_IF_ERROR(CorrectionsFor(st, key, hierarchy_level, &corr));
+  hipStream_t s = ThreadStream();
+
+  const int bbits = log_domain_size - m.tree_level;
+  std::vector<uint128> tree(n);
+  std::vector<uint8_t> bidx(n, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    tree[i] = m.epb > 1 ? (evaluation_points[i] >> bbits) : evaluation_points[i];
+    if (m.epb > 1) bidx[i] = static_cast<uint8_t>(evaluation_points[i] & ((uint128{1} << bbits) - 1));
+  }
+  DeviceBuffer seeds, cbs, paths, bi, cws, ccl, ccr, dout;
+  int start_level = 0;
+  if (ctx == nullptr) {
+    std::vector<uint128> sv(n, MakeUint128(key.seed().high(), key.seed().low()));
+    std::vector<uint8_t> cv(n, static_cast<uint8_t>(key.party() != 0));
+    DPF_RETURN_IF_ERROR(seeds.Upload(sv.data(), 16 * n, s));
+    DPF_RETURN_IF_ERROR(cbs.Upload(cv.data(), n, s));
+  } else {
+    DPF_RETURN_IF_ERROR(ComputePartialEvaluations(st, Span<const uint128>(tree.data(), n),
+                                                  hierarchy_level, true, *ctx, s, &seeds, &cbs));
+    start_level = m.tree_level;
+  }
+  const int levels = m.tree_level - start_level;
+  CwArrays cw = KeyCws(key, start_level, m.tree_level);
+  DPF_RETURN_IF_ERROR(paths.Upload(tree.data(), 16 * n, s));
+  DPF_RETURN_IF_ERROR(bi.Upload(bidx.data(), n, s));
+  DPF_RETURN_IF_ERROR(cws.Upload(cw.seeds.data(), 16 * levels, s));
+  DPF_RETURN_IF_ERROR(ccl.Upload(cw.ccl.data(), levels, s));
+  DPF_RETURN_IF_ERROR(ccr.Upload(cw.ccr.data(), levels, s));
+  DPF_RETURN_IF_ERROR(dout.Alloc(n * vt.out_stride, s));
+  DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_points(
+      n, seeds.get(), cbs.as<uint8_t>(), paths.get(), 0, levels, levels, cws.get(),
+      ccl.as<uint8_t>(), ccr.as<uint8_t>(), &vt, bi.as<uint8_t>(), nullptr, key.party(), nullptr,
+      reinterpret_cast<const uint64_t*>(corr.data()), dout.get(), nullptr, nullptr, s)));
+  DPF_RETURN_IF_ERROR(HipStatus(
+      hipMemcpyAsync(out, dout.get(), n * vt.out_stride, hipMemcpyDeviceToHost, s), "d2h"));
+  DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+  if (ctx) ctx->set_previous_hierarchy_level(hierarchy_level);
+  return OkStatus();
+}
+
+Status DistributedPointFunction::EvaluateAndApplyRaw(Span<const DpfKey* const> keys,
+                                                     Span<const uint128> evaluation_points,
+                                                     int rightshift,
+                                                     const dpf_amd_value_type& layout,
+                                                     void* out, int* levels_done) const {
+  const DpfState& st = *state_;
+  if (evaluation_points.size() != keys.size())
+    return InvalidArgumentError("`keys.size()` != `evaluation_points.size()`");
+  for (size_t i = 0; i < keys.size(); ++i) DPF_RETURN_IF_ERROR(ValidateDpfKey(st, *keys[i]));
+  const int64_t n = static_cast<int64_t>(keys.size());
+  const int H = num_hierarchy_levels();
+  *levels_done = 0;
+  if (n == 0) return OkStatus();
+  hipStream_t s = ThreadStream();
+  std::vector<uint128> sv(n);
+  std::vector<uint8_t> cv(n);
+  std::vector<int8_t> party(n);
+  for (int64_t i = 0; i < n; ++i) {
+    sv[i] = MakeUint128(keys[i]->seed().high(), keys[i]->seed().low());
+    cv[i] = static_cast<uint8_t>(keys[i]->party() != 0);
+    party[i] = static_cast<int8_t>(keys[i]->party());
+  }
+  DeviceBuffer seeds, cbs, paths, pty, dout;
+  DPF_RETURN_IF_ERROR(seeds.Upload(sv.data(), 16 * n, s));
+  DPF_RETURN_IF_ERROR(cbs.Upload(cv.data(), n, s));
+  DPF_RETURN_IF_ERROR(paths.Upload(evaluation_points.data(), 16 * n, s));
+  DPF_RETURN_IF_ERROR(pty.Upload(party.data(), n, s));
+  const int last_ld = st.parameters.back().log_domain_size();
+  int start_level = 0, stop_level = st.hierarchy_to_tree[0];
+  char* host_out = static_cast<char*>(out);
+  for (int h = 0; h < H; ++h) {
+    if (h > 0) {
+      start_level = stop_level;
+      stop_level = st.hierarchy_to_tree[h];
+    }
+    const LevelMeta& m = st.levels[h];
+    dpf_amd_value_type vt;
+    DPF_RETURN_IF_ERROR(MergeLayout(m, layout, &vt));
+    const int domain_rs = rightshift + last_ld - m.log_domain;
+    const int tree_rs = rightshift + last_ld - m.tree_level;
+    const int levels = stop_level - start_level;
+    std::vector<uint128> cws(static_cast<size_t>(levels) * n);
+    std::vector<uint8_t> ccl(cws.size()), ccr(cws.size()), bidx(n, 0);
+    for (int l = 0; l < levels; ++l)
+      for (int64_t j = 0; j < n; ++j) {
+        const CorrectionWord& cw = keys[j]->correction_words(start_level + l);
+        cws[l * n + j] = MakeUint128(cw.seed().high(), cw.seed().low());
+        ccl[l * n + j] = cw.control_left();
+        ccr[l * n + j] = cw.control_right();
+      }
+    const int per = m.epb * static_cast<int>(m.scalars.size());
+    std::vector<uint128> corr(static_cast<size_t>(per) * n);
+    std::vector<uint128> tmp;
+    const int bbits = m.log_domain - m.tree_level;
+    for (int64_t j = 0; j < n; ++j) {
+      DPF_RETURN_IF_ERROR(CorrectionsFor(st, *keys[j], h, &tmp));
+      std::copy(tmp.begin(), tmp.end(), corr.begin() + j * per);
+      if (m.epb > 1 && domain_rs < 128)
+        bidx[j] = static_cast<uint8_t>((evaluation_points[j] >> domain_rs) &
+                                       ((uint128{1} << bbits) - 1));
+    }
+    DeviceBuffer dcws, dccl, dccr, dcorr, dbi;
+    DPF_RETURN_IF_ERROR(dcws.Upload(cws.data(), 16 * cws.size(), s));
+    DPF_RETURN_IF_ERROR(dccl.Upload(ccl.data(), ccl.size(), s));
+    DPF_RETURN_IF_ERROR(dccr.Upload(ccr.data(), ccr.size(), s));
+    DPF_RETURN_IF_ERROR(dcorr.Upload(corr.data(), 16 * corr.size(), s));
+    DPF_RETURN_IF_ERROR(dbi.Upload(bidx.data(), n, s));
+    DPF_RETURN_IF_ERROR(dout.Alloc(n * vt.out_stride, s));
+    DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_points(
+        n, seeds.get(), cbs.as<uint8_t>(), paths.get(), std::min(tree_rs, 255), levels,
+        static_cast<int64_t>(levels) * n, dcws.get(), dccl.as<uint8_t>(), dccr.as<uint8_t>(),
+        &vt, dbi.as<uint8_t>(), pty.as<int8_t>(), 0, dcorr.get(), nullptr, dout.get(),
+        seeds.get(), cbs.as<uint8_t>(), s)));
+    DPF_RETURN_IF_ERROR(HipStatus(hipMemcpyAsync(host_out + h * n * vt.out_stride, dout.get(),
+                                                 n * vt.out_stride, hipMemcpyDeviceToHost, s),
+                                  "d2h"));
+    DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+    *levels_done = h + 1;
+  }
+  return OkStatus();
+}
+
+Status DistributedPointFunction::ExpandLeavesOnDevice(const DpfKey& key, int64_t leaf_begin,
+                                                      int64_t leaf_end,
+                                                      const dpf_amd_value_type& layout,
+                                                      void* out, void* stream) const {
+  const DpfState& st = *state_;
+  DPF_RETURN_IF_ERROR(ValidateDpfKey(st, key));
+  const int h = num_hierarchy_levels() - 1;
+  const LevelMeta& m = st.levels[h];
+  if (m.tree_level > 62) return InvalidArgumentError("domain too large to expand fully");
+  dpf_amd_value_type vt;
+  DPF_RETURN_IF_ERROR(MergeLayout(m, layout, &vt));
+  std::vector<uint128> corr;
+  DPF_RETURN_IF_ERROR(CorrectionsFor(st, key, h, &corr));
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ThreadStream();
+  const uint128 seed = MakeUint128(key.seed().high(), key.seed().low());
+  const uint8_t cb = static_cast<uint8_t>(key.party() != 0);
+  CwArrays cw = KeyCws(key, 0, m.tree_level);
+  DeviceBuffer rs, rc, cws, ccl, ccr;
+  DPF_RETURN_IF_ERROR(rs.Upload(&seed, 16, s));
+  DPF_RETURN_IF_ERROR(rc.Upload(&cb, 1, s));
+  DPF_RETURN_IF_ERROR(cws.Upload(cw.seeds.data(), 16 * m.tree_level, s));
+  DPF_RETURN_IF_ERROR(ccl.Upload(cw.ccl.data(), m.tree_level, s));
+  DPF_RETURN_IF_ERROR(ccr.Upload(cw.ccr.data(), m.tree_level, s));
+  const int cepb = 1 << (m.log_domain - m.tree_level);
+  return AbiStatus(dpf_amd_expand_and_correct(
+      1, rs.get(), rc.as<uint8_t>(), m.tree_level, cws.get(), ccl.as<uint8_t>(),
+      ccr.as<uint8_t>(), &vt, reinterpret_cast<const uint64_t*>(corr.data()), key.party(), cepb,
+      leaf_begin, leaf_end, out, s));
+}
+
+}  // namespace distributed_point_functions
