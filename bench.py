@@ -216,7 +216,7 @@ def cpu_baseline(args):
         leaves += 1 << log_blocks
         i += 1
         el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or i >= 64:
+        if el >= args.cpu_seconds or i >= 4096:
             break
     return dict(value=leaves / el, unit="leaves/s", cores=1, kind="port",
                 sample="%d x 2^%d-leaf subtrees of the c5 key (%.1f s), oracle/dpf_oracle.c "

@@ -66,6 +66,13 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: torch bundles its own libamdhip64.so.7;
+    # loading it first makes libdpf_amd.so bind to the same runtime (same
+    # soname) instead of pulling in a second copy from /opt/rocm.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             "native library %s is missing; build it with "
