@@ -7,9 +7,10 @@ Headline (`value`): full-domain DPF evaluation leaves/s over the whole job —
 config c5 of BASELINE.json: one key, log_domain_size = 32,
 Tuple<uint32, IntModN<uint64, 2^64-59>>, security_parameter = 48
 (EvaluateNext({}, ctx), dpf/distributed_point_function.h:695-891), 2^32
-leaves per step, outputs kept in HBM in the host layout of the type.  With N
-ranks the 2^32-leaf domain is split into N disjoint subtree slices (strong
-scaling, no collective on the data path).
+leaves per step per rank, outputs kept in HBM in the host layout of the type.
+With N ranks every rank evaluates the full 2^32-leaf domain of its own key
+(independent keys are independent objects: weak scaling, no collective on
+the data path); `value` = N * 2^32 leaves / max-over-ranks step time.
 
 Secondary (`pir`): dense PIR config c4 — 2^26 records x 256 B, one query:
 the selection DPF (only the ceil(N/128) leaves the scan reads) + the XOR
@@ -98,14 +99,15 @@ def bench_dpf(args, world, rank, device):
     log_domain = args.log_domain
     dpf = DistributedPointFunction.create(DpfParameters(log_domain, vt, 48))
     alpha = 0x9E3779B9 % (1 << log_domain)
-    k0, _ = dpf.generate_keys(alpha, (123456789, 987654321), seeds=(0xA5A5, 0x5A5A))
+    # one key per rank (rank 0's key is the one the CPU baseline times)
+    k0, _ = dpf.generate_keys(alpha, (123456789, 987654321),
+                              seeds=(0xA5A5 + 2 * rank, 0x5A5A + 2 * rank))
     ka = key_arrays(dpf, k0, 0, device)
     desc = dpf.value_type_descriptor(0)
     L = ka["L"]
     cepb = 1 << (log_domain - L)
     total = 1 << L
-    per = total // world
-    lo, hi = rank * per, (rank + 1) * per if rank < world - 1 else total
+    lo, hi = 0, total
     out = torch.empty((hi - lo) * cepb * desc.out_stride, dtype=torch.uint8, device=device)
 
     def step():
@@ -128,8 +130,7 @@ def bench_dpf(args, world, rank, device):
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
     wall = max_over_ranks(wall, world)
     kernel_ms = max_over_ranks(kernel_ms, world)
-    leaves = total * cepb
-    # spot-check a few outputs against the second key's share (share-sum)
+    leaves = total * cepb * world
     return dict(wall=wall, kernel_ms=kernel_ms, leaves=leaves, L=L, lo=lo, hi=hi)
 
 
@@ -197,6 +198,22 @@ def bench_pir(args, world, rank, device):
                 records=n)
 
 
+def traffic_from_profiles(kernel_substr):
+    """HBM bytes per launch of a kernel from the newest committed PMC summary
+    (profiles/<round>_pmc.json, written by tools/summarize_profile.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                          "profiles", "r*_pmc.json")))
+    for f in reversed(files):
+        with open(f) as fh:
+            d = json.load(fh)
+        for name, e in d.items():
+            if kernel_substr in name and "hbm_bytes" in e:
+                return e["hbm_bytes"]
+    return None
+
+
 def cpu_baseline(args):
     """Oracle (reference CPU algorithm restated in C, AES-NI, 1 thread) on a
     bounded slice of the c5 workload: subtrees of 2^20 leaves of the same
@@ -245,21 +262,25 @@ def main():
         leaves = r["leaves"]
         ms = 1000 * r["wall"] / args.steps
         value = leaves / (r["wall"] / args.steps)
-        aes_per_launch = AES_PER_LEAF_C5 * leaves / world
+        aes_per_launch = AES_PER_LEAF_C5 * leaves / world  # one launch per rank per step
         aes_s = aes_per_launch / (r["kernel_ms"] / 1e3)
         achieved = aes_s * OPS_PER_AES / 1e12
         out = {
             "metric": METRIC, "value": value, "unit": "leaves/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "u32", "data": "synthetic (fixed-seed DPF key)",
             "config": {"workload": "c5: full-domain EvaluateNext, log_domain_size=%d, "
                                    "Tuple<uint32,IntModN<uint64,2^64-59>>, "
                                    "security_parameter=48" % args.log_domain,
                        "leaves_per_step": leaves, "tree_levels": r["L"],
-                       "parallelism": "subtree-sharded x%d" % world},
+                       "parallelism": "independent keys, one 2^%d domain per GPU x%d" %
+                                      (args.log_domain, world)},
             "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS,
-                         "unit": "TOP/s", "frac": achieved / VALU_PEAK_TOPS, "traffic": None,
+                         "unit": "TOP/s", "frac": achieved / VALU_PEAK_TOPS,
+                         "traffic": traffic_from_profiles("KExpand<8, dpf_amd::EmitU32ModN64>"),
+                         "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/)",
+                         "algorithmic_bytes": leaves // world * 16,
                          "kernel": "KExpand<8,EmitU32ModN64>", "kernel_ms": r["kernel_ms"],
                          "aes_per_s_per_gpu": aes_s,
                          "ops_per_aes": OPS_PER_AES,
@@ -277,8 +298,11 @@ def main():
                             "(selection DPF + XOR scan%s)" %
                             (pir["records"], " + RCCL all-gather + fold" if world > 1 else ""),
                 "ms_per_query": 1e3 * pir["wall_s"], "correct": pir["ok"],
+                "scaling": "strong",
                 "roofline": {"bound": "hbm", "achieved": scan_gbs, "peak": HBM_PEAK_GBS,
-                             "unit": "GB/s", "frac": scan_gbs / HBM_PEAK_GBS, "traffic": None,
+                             "unit": "GB/s", "frac": scan_gbs / HBM_PEAK_GBS,
+                             "traffic": traffic_from_profiles("KPirScan<1>"),
+                             "algorithmic_bytes": pir["per_gpu_bytes"],
                              "kernel": "KPirScan<1>+KXorFold", "kernel_ms": pir["scan_ms"]},
             }
         print(json.dumps(out), flush=True)

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
 #include <cstring>
 #include <string>
 
@@ -26,11 +27,6 @@ constexpr int kTabWords = 256 * 64;  // 64 KiB
 constexpr int kBlock = 256;  // 64 KiB LDS table per block; 2 blocks per CU
 
 __constant__ Te0Table c_te0 = MakeTe0();
-// DPF PRG keys (cc:55-60): [left, right, value].
-__constant__ AesKey c_dpf_keys[3] = {
-    ExpandAesKey(kPrgKeyLeftLo, kPrgKeyLeftHi),
-    ExpandAesKey(kPrgKeyRightLo, kPrgKeyRightHi),
-    ExpandAesKey(kPrgKeyValueLo, kPrgKeyValueHi)};
 
 struct KeyPair {
   AesKey k[2];
@@ -71,23 +67,35 @@ __device__ __forceinline__ uint32_t Rotl16(uint32_t x) {
   return __builtin_amdgcn_alignbit(x, x, 16);
 }
 
+__device__ __forceinline__ uint32_t Xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // one v_bitop3_b32
+}
+
+// The three DPF PRG keys (cc:55-60) expanded at compile time.  Device code
+// indexes them with unrolled constant indices, so every round-key word is a
+// literal materialised by s_mov (SALU) next to its use: no constant-memory
+// loads, no SGPR pressure, no VGPR-lane spills of hoisted keys.
+constexpr AesKey kDpfKeys[3] = {ExpandAesKey(kPrgKeyLeftLo, kPrgKeyLeftHi),
+                                ExpandAesKey(kPrgKeyRightLo, kPrgKeyRightHi),
+                                ExpandAesKey(kPrgKeyValueLo, kPrgKeyValueHi)};
+
 // Key accessors: rk(n, i) / rkr(n, i) for state n, round-key word i.
+template <int W>
 struct DpfKeyAt {  // one fixed DPF key for all states
-  int which;
-  __device__ __forceinline__ uint32_t rk(int, int i) const { return c_dpf_keys[which].rk[i]; }
-  __device__ __forceinline__ uint32_t rkr(int, int i) const { return c_dpf_keys[which].rkr[i]; }
+  __device__ __forceinline__ uint32_t rk(int, int i) const { return kDpfKeys[W].rk[i]; }
+  __device__ __forceinline__ uint32_t rkr(int, int i) const { return kDpfKeys[W].rkr[i]; }
 };
 struct DpfLeftRight {  // state 0: left key, state 1: right key
-  __device__ __forceinline__ uint32_t rk(int n, int i) const { return c_dpf_keys[n].rk[i]; }
-  __device__ __forceinline__ uint32_t rkr(int n, int i) const { return c_dpf_keys[n].rkr[i]; }
+  __device__ __forceinline__ uint32_t rk(int n, int i) const { return kDpfKeys[n].rk[i]; }
+  __device__ __forceinline__ uint32_t rkr(int n, int i) const { return kDpfKeys[n].rkr[i]; }
 };
 struct DpfSelect {  // per-lane choice of the left / right key (path walk)
   bool right;
   __device__ __forceinline__ uint32_t rk(int, int i) const {
-    return right ? c_dpf_keys[1].rk[i] : c_dpf_keys[0].rk[i];
+    return right ? kDpfKeys[1].rk[i] : kDpfKeys[0].rk[i];
   }
   __device__ __forceinline__ uint32_t rkr(int, int i) const {
-    return right ? c_dpf_keys[1].rkr[i] : c_dpf_keys[0].rkr[i];
+    return right ? kDpfKeys[1].rkr[i] : kDpfKeys[0].rkr[i];
   }
 };
 struct PairSelect {  // generic keys from a kernel argument
@@ -101,8 +109,11 @@ struct PairSelect {  // generic keys from a kernel argument
   }
 };
 
-// N independent AES-128 encryptions in lockstep (16N independent LDS lookups
-// per round for latency hiding).
+// N independent AES-128 encryptions in lockstep.  Each round first forms all
+// 16N table addresses (v_perm), then issues all 16N ds_read_b32 back to back
+// (sched_group_barrier keeps the scheduler from splitting them into small
+// waitcnt-separated groups), then combines: per output column
+// T0[a] ^ T1[b] ^ rotl16(T0[c] ^ T1[d] ^ rotr16(rk)) = 2 v_bitop3 + 1 alignbit.
 template <int N, class K>
 __device__ __forceinline__ void AesN(uint32_t (&w)[N][4], const K& key,
                                      const Lds& L) {
@@ -112,42 +123,46 @@ __device__ __forceinline__ void AesN(uint32_t (&w)[N][4], const K& key,
     for (int c = 0; c < 4; ++c) w[n][c] ^= key.rk(n, c);
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
-    uint32_t o[N][4];
-#pragma unroll
-    for (int n = 0; n < N; ++n) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        uint32_t a = LoadT0(L, w[n][c], 0);
-        uint32_t b = LoadT1(L, w[n][(c + 1) & 3], 1);
-        uint32_t cc = LoadT0(L, w[n][(c + 2) & 3], 2);
-        uint32_t d = LoadT1(L, w[n][(c + 3) & 3], 3);
-        o[n][c] = a ^ b ^ Rotl16(cc ^ d ^ key.rkr(n, 4 * r + c));
-      }
-    }
+    uint32_t t[N][4][4];
 #pragma unroll
     for (int n = 0; n < N; ++n)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) w[n][c] = o[n][c];
+      for (int c = 0; c < 4; ++c) {
+        t[n][c][0] = LoadT0(L, w[n][c], 0);
+        t[n][c][1] = LoadT1(L, w[n][(c + 1) & 3], 1);
+        t[n][c][2] = LoadT0(L, w[n][(c + 2) & 3], 2);
+        t[n][c][3] = LoadT1(L, w[n][(c + 3) & 3], 3);
+      }
+    __builtin_amdgcn_sched_group_barrier(0x002, 16 * N, 0);  // address VALU
+    __builtin_amdgcn_sched_group_barrier(0x100, 16 * N, 0);  // DS reads
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        w[n][c] = Xor3(t[n][c][0], t[n][c][1],
+                       Rotl16(Xor3(t[n][c][2], t[n][c][3], key.rkr(n, 4 * r + c))));
   }
   // Last round: S-box bytes are byte 1/2 of T0 and byte 3 of T1.
-  uint32_t o[N][4];
-#pragma unroll
-  for (int n = 0; n < N; ++n) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      uint32_t a = LoadT0(L, w[n][c], 0);
-      uint32_t b = LoadT0(L, w[n][(c + 1) & 3], 1);
-      uint32_t cc = LoadT0(L, w[n][(c + 2) & 3], 2);
-      uint32_t d = LoadT1(L, w[n][(c + 3) & 3], 3);
-      uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0c0c0501u);
-      uint32_t hi = __builtin_amdgcn_perm(d, cc, 0x07020c0cu);
-      o[n][c] = lo ^ hi ^ key.rk(n, 40 + c);
-    }
-  }
+  uint32_t t[N][4][4];
 #pragma unroll
   for (int n = 0; n < N; ++n)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) w[n][c] = o[n][c];
+    for (int c = 0; c < 4; ++c) {
+      t[n][c][0] = LoadT0(L, w[n][c], 0);
+      t[n][c][1] = LoadT0(L, w[n][(c + 1) & 3], 1);
+      t[n][c][2] = LoadT0(L, w[n][(c + 2) & 3], 2);
+      t[n][c][3] = LoadT1(L, w[n][(c + 3) & 3], 3);
+    }
+  __builtin_amdgcn_sched_group_barrier(0x002, 16 * N, 0);
+  __builtin_amdgcn_sched_group_barrier(0x100, 16 * N, 0);
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t lo = __builtin_amdgcn_perm(t[n][c][1], t[n][c][0], 0x0c0c0501u);
+      const uint32_t hi = __builtin_amdgcn_perm(t[n][c][3], t[n][c][2], 0x07020c0cu);
+      w[n][c] = Xor3(lo, hi, key.rk(n, 40 + c));
+    }
 }
 
 // sigma(x) = (x.hi ^ x.lo, x.hi) (aes_128_fixed_key_hash.cc:75-78) in words.
@@ -333,7 +348,7 @@ __device__ __forceinline__ void HashSeeds(const uint32_t (&x)[NS][4], u128 (&W)[
       for (int c = 0; c < 4; ++c) st[n * BN + j][c] = sg[n * BN + j][c];
     }
   }
-  AesN<NS * BN>(st, DpfKeyAt{2}, L);
+  AesN<NS * BN>(st, DpfKeyAt<2>{}, L);
 #pragma unroll
   for (int i = 0; i < NS * BN; ++i) {
 #pragma unroll
@@ -455,7 +470,7 @@ __device__ __forceinline__ void HashWords(const uint32_t (&x)[NS][4],
       for (int c = 0; c < 4; ++c) st[n * BN + j][c] = sg[n * BN + j][c];
     }
   }
-  AesN<NS * BN>(st, DpfKeyAt{2}, L);
+  AesN<NS * BN>(st, DpfKeyAt<2>{}, L);
 #pragma unroll
   for (int n = 0; n < NS; ++n)
 #pragma unroll
@@ -810,19 +825,47 @@ __global__ void KGatherRows(int64_t n, const int64_t* src_offset, int64_t opp,
   }
 }
 
-__global__ void KXorFold(const uint4* parts, int num_parts, int64_t words, uint4* out) {
-  const int64_t step = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += step) {
-    uint4 acc = make_uint4(0, 0, 0, 0);
-    for (int p = 0; p < num_parts; ++p) {
-      uint4 v = parts[(int64_t)p * words + i];
+// XOR of num_parts equally sized partial vectors.  A 256-thread block owns
+// kFoldWords consecutive 16-byte words; its threads split the parts into
+// kFoldSlices interleaved slices (loads of one part stay contiguous), then the
+// slices are folded through LDS.  Keeps many independent loads in flight, so
+// a 2048-part fold of a few hundred bytes costs microseconds, not a serial
+// chain of 2048 dependent loads.
+constexpr int kFoldWords = 4;
+constexpr int kFoldSlices = 64;
+
+__global__ __launch_bounds__(256) void KXorFold(const uint4* parts, int num_parts,
+                                                int64_t words, uint4* out) {
+  __shared__ uint4 red[kFoldSlices][kFoldWords];
+  const int w = threadIdx.x % kFoldWords;
+  const int s = threadIdx.x / kFoldWords;
+  const int64_t i = (int64_t)blockIdx.x * kFoldWords + w;
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  if (i < words) {
+#pragma unroll 8
+    for (int p = s; p < num_parts; p += kFoldSlices) {
+      const uint4 v = parts[(int64_t)p * words + i];
       acc.x ^= v.x;
       acc.y ^= v.y;
       acc.z ^= v.z;
       acc.w ^= v.w;
     }
-    out[i] = acc;
   }
+  red[s][w] = acc;
+  __syncthreads();
+  for (int half = kFoldSlices / 2; half > 0; half >>= 1) {
+    if (s < half) {
+      const uint4 o = red[s + half][w];
+      uint4 m = red[s][w];
+      m.x ^= o.x;
+      m.y ^= o.y;
+      m.z ^= o.z;
+      m.w ^= o.w;
+      red[s][w] = m;
+    }
+    __syncthreads();
+  }
+  if (s == 0 && i < words) out[i] = red[0][w];
 }
 
 __global__ void KXorFoldBytes(const uint8_t* parts, int num_parts, int64_t bytes,
@@ -1281,7 +1324,9 @@ int dpf_amd_xor_fold(const void* parts, int num_parts, int64_t bytes, void* out,
   hipStream_t st = (hipStream_t)stream;
   if (bytes % 16 == 0 && ((uintptr_t)parts % 16 == 0) && ((uintptr_t)out % 16 == 0)) {
     const int64_t words = bytes / 16;
-    hipLaunchKernelGGL(KXorFold, dim3(GridFor(words, 256, 4096)), dim3(256), 0, st,
+    const int64_t blocks = (words + kFoldWords - 1) / kFoldWords;
+    if (blocks > INT32_MAX) return SetError(DPF_AMD_INVALID_ARGUMENT, "xor fold too large");
+    hipLaunchKernelGGL(KXorFold, dim3((unsigned)blocks), dim3(256), 0, st,
                        (const uint4*)parts, num_parts, words, (uint4*)out);
   } else {
     hipLaunchKernelGGL(KXorFoldBytes, dim3(GridFor(bytes, 256, 4096)), dim3(256), 0, st,

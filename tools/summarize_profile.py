@@ -1,0 +1,86 @@
+"""Summarise a tools/profile_gpu.sh run into profiles/.
+
+Usage: python tools/summarize_profile.py <tag>
+
+Reads gpurun_out/prof_<tag>/ (trace pass + PMC passes) and writes
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
+  profiles/<tag>_pmc.json           per-kernel, per-launch counter averages and
+                                    corrected HBM bytes
+  profiles/<tag>_summary.md         human-readable table
+
+HBM bytes follow MI355X_MICROARCH.md (HBM / rocprofv3 section): FETCH_SIZE and
+WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
+(16 B/lane) coalesced streaming read, so it is doubled; WRITE_SIZE is exact
+for 16-B-per-lane stores.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    name = name.replace("dpf_amd::", "")
+    if name.startswith("void "):
+        name = name[5:]
+    return name.split("(")[0] if "(" in name and "<" not in name.split("(")[0][-1:] else name[:80]
+
+
+def main(tag):
+    src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
+    kstats = {}
+    if stats:
+        shutil.copy(stats[0], os.path.join(dst, tag + "_kernel_stats.csv"))
+        for r in csv.DictReader(open(stats[0])):
+            kstats[r["Name"]] = r
+    pmc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(src, "pmc_*", "*counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            if "dpf_amd" not in r["Kernel_Name"]:
+                continue
+            pmc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {}
+    for k, d in pmc.items():
+        avg = {c: sum(v) / len(v) for c, v in d.items()}
+        e = {"counters_per_launch": avg, "launches": max(len(v) for v in d.values())}
+        if "FETCH_SIZE" in avg:
+            e["hbm_read_bytes"] = avg["FETCH_SIZE"] * 1024 * 2
+        if "WRITE_SIZE" in avg:
+            e["hbm_write_bytes"] = avg["WRITE_SIZE"] * 1024
+        if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+            e["hbm_bytes"] = e["hbm_read_bytes"] + e["hbm_write_bytes"]
+        if k in kstats:
+            e["avg_duration_ns"] = float(kstats[k]["AverageNs"])
+            e["calls_in_trace"] = int(kstats[k]["Calls"])
+        if "SQ_INSTS_VALU" in avg and "SQ_INSTS_LDS" in avg:
+            e["lds_per_valu"] = avg["SQ_INSTS_LDS"] / max(avg["SQ_INSTS_VALU"], 1)
+        out[k] = e
+    with open(os.path.join(dst, tag + "_pmc.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    lines = ["# Profile %s" % tag, "",
+             "Source: `bash tools/profile_gpu.sh %s` on one MI355X (trace pass "
+             "`rocprofv3 --kernel-trace --stats`, then separate `--pmc` passes)." % tag, "",
+             "| kernel | calls | avg ms | HBM read GB | HBM write GB | VALU wave-instr | LDS wave-instr | LDS bank conflicts |",
+             "|---|---|---|---|---|---|---|---|"]
+    for k, e in sorted(out.items(), key=lambda kv: -kv[1].get("avg_duration_ns", 0)):
+        c = e["counters_per_launch"]
+        lines.append("| `%s` | %s | %.3f | %.3f | %.3f | %.4g | %.4g | %.4g |" % (
+            k[:90], e.get("calls_in_trace", "?"), e.get("avg_duration_ns", 0) / 1e6,
+            e.get("hbm_read_bytes", 0) / 1e9, e.get("hbm_write_bytes", 0) / 1e9,
+            c.get("SQ_INSTS_VALU", 0), c.get("SQ_INSTS_LDS", 0),
+            c.get("SQ_LDS_BANK_CONFLICT", 0)))
+    with open(os.path.join(dst, tag + "_summary.md"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
