@@ -33,7 +33,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from distributed_point_functions_amd import _lib, kernels
+from distributed_point_functions_amd import _lib, kernels, sharding
 from distributed_point_functions_amd import value_types as V
 from distributed_point_functions_amd.dpf import DistributedPointFunction, DpfParameters, decode_value
 
@@ -137,8 +137,8 @@ def bench_dpf(args, world, rank, device):
 def bench_pir(args, world, rank, device):
     n = 1 << args.pir_log_records
     rec = 256
-    per = n // world
-    r_lo = rank * per
+    r_lo, r_hi, b_lo, b_hi = sharding.pir_row_shard(n, world, rank)
+    per = r_hi - r_lo
     gen = torch.Generator(device=device)
     gen.manual_seed(1234 + rank)
     db = torch.randint(0, 256, (per * rec,), dtype=torch.uint8, device=device, generator=gen)
@@ -146,16 +146,12 @@ def bench_pir(args, world, rank, device):
     dpf = DistributedPointFunction.create(DpfParameters(log_domain, V.XorWrapper(128)))
     idx = (n * 3) // 7 + 5
     k0, k1 = dpf.generate_keys(idx // 128, 1 << (idx % 128), seeds=(0x1111, 0x2222))
-    nb = n // 128
-    b_lo, b_hi = r_lo // 128, (r_lo + per) // 128
     desc = dpf.value_type_descriptor(0)
     keys = [key_arrays(dpf, k, 0, device) for k in (k0, k1)]
-    sel = torch.empty((b_hi - b_lo) * 16, dtype=torch.uint8, device=device)
+    sel = torch.empty(max(1, b_hi - b_lo) * 16, dtype=torch.uint8, device=device)
     ws = torch.empty(max(16, _lib.lib().dpf_amd_inner_product_workspace_size(per, rec, 1)),
                      dtype=torch.uint8, device=device)
     part = torch.empty(rec, dtype=torch.uint8, device=device)
-    gathered = torch.empty(world * rec, dtype=torch.uint8, device=device)
-    result = torch.empty(rec, dtype=torch.uint8, device=device)
     scan_ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 
     def query(ka, timed_scan=False):
@@ -166,18 +162,13 @@ def bench_pir(args, world, rank, device):
         kernels.inner_product(db, per, rec, sel.view(torch.int64).view(-1, 2), 1, ws, part)
         if timed_scan:
             scan_ev[1].record()
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, part)
-            kernels.xor_fold(gathered, world, rec, result)
-            return result
-        return part
+        return sharding.allgather_xor(part, world)
 
     # correctness: share0 ^ share1 == record idx (held by its owner rank)
     a = query(keys[0]).clone()
     b = query(keys[1]).clone()
     rec_idx = torch.zeros(rec, dtype=torch.uint8, device=device)
-    owner = idx // per
-    if owner == rank:
+    if r_lo <= idx < r_hi:
         rec_idx.copy_(db[(idx - r_lo) * rec:(idx - r_lo + 1) * rec])
     if world > 1:
         dist.all_reduce(rec_idx, op=dist.ReduceOp.SUM)

@@ -18,6 +18,7 @@ OUT_DIR = os.path.join(PKG, "_native")
 OBJ_DIR = os.path.join(OUT_DIR, "obj")
 LIB = os.path.join(OUT_DIR, "libdpf_amd.so")
 ARCH = os.environ.get("DPF_AMD_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
             "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
@@ -44,7 +45,9 @@ def _compile(src: str, force: bool) -> str:
     if src.endswith(".hip"):
         cmd[1:1] = ["--offload-arch=" + ARCH, "-x", "hip"]
     else:
-        cmd[1:1] = ["-maes", "-msse4.1"]
+        # host-only C++ (no device pass), HIP runtime API from ROCm
+        cmd[1:1] = ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(ROCM, "include"),
+                    "-maes", "-msse4.1"]
     subprocess.check_call(cmd)
     os.replace(obj + ".tmp", obj)
     return obj

@@ -3,6 +3,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -293,22 +294,124 @@ int dpf_amd_pir_db_inner_product(const dpf_amd_pir_db* db, const uint64_t* selec
   return DPF_AMD_OK;
 }
 
-int dpf_amd_pir_server_create_plain(const uint8_t* config, size_t config_len, dpf_amd_pir_db* db,
-                                    dpf_amd_pir_server** out) {
-  PirConfig c;
-  if (!c.ParseFromArray(config, config_len))
+}  // extern "C"
+
+struct dpf_amd_pir_call {
+  std::function<void()>* while_waiting = nullptr;
+  bool waited = false;
+  bool has_response = false;
+  std::string response;
+};
+
+namespace {
+
+// Shared by the three factories: parses the config, finishes the database.
+int PrepareServer(const uint8_t* config, size_t config_len, dpf_amd_pir_db* db, PirConfig* c,
+                  std::unique_ptr<DenseDpfPirServer::Database>* d) {
+  if (!c->ParseFromArray(config, config_len)) {
+    delete db;
     return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed PirConfig proto");
+  }
   if (db && !db->built) {
     int rc = dpf_amd_pir_db_build(db);
-    if (rc != DPF_AMD_OK) return rc;
+    if (rc != DPF_AMD_OK) {
+      delete db;
+      return rc;
+    }
   }
-  std::unique_ptr<DenseDpfPirServer::Database> d;
-  if (db) d = std::move(db->built);
-  StatusOr<std::unique_ptr<DenseDpfPirServer>> s = DenseDpfPirServer::CreatePlain(c, std::move(d));
+  if (db) *d = std::move(db->built);
   delete db;
+  return DPF_AMD_OK;
+}
+
+int Finish(StatusOr<std::unique_ptr<DenseDpfPirServer>> s, dpf_amd_pir_server** out) {
   if (!s.ok()) return Fail(s.status());
   *out = new dpf_amd_pir_server{std::move(*s)};
   return DPF_AMD_OK;
+}
+
+Status CallbackStatus(int rc, const char* what) {
+  return Status(static_cast<StatusCode>(rc == DPF_AMD_OK ? DPF_AMD_INTERNAL : rc),
+                std::string(what) + " callback failed with status " + std::to_string(rc));
+}
+
+}  // namespace
+
+extern "C" {
+
+int dpf_amd_pir_call_while_waiting(dpf_amd_pir_call* call) {
+  if (!call || !call->while_waiting)
+    return Fail(DPF_AMD_FAILED_PRECONDITION, "no `while_waiting` for this call");
+  if (call->waited) return Fail(DPF_AMD_FAILED_PRECONDITION, "`while_waiting` already called");
+  call->waited = true;
+  (*call->while_waiting)();
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_pir_call_set_response(dpf_amd_pir_call* call, const uint8_t* data, size_t len) {
+  if (!call) return Fail(DPF_AMD_INVALID_ARGUMENT, "null call");
+  call->response.assign(reinterpret_cast<const char*>(data), len);
+  call->has_response = true;
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_pir_server_create_plain(const uint8_t* config, size_t config_len, dpf_amd_pir_db* db,
+                                    dpf_amd_pir_server** out) {
+  PirConfig c;
+  std::unique_ptr<DenseDpfPirServer::Database> d;
+  int rc = PrepareServer(config, config_len, db, &c, &d);
+  if (rc != DPF_AMD_OK) return rc;
+  return Finish(DenseDpfPirServer::CreatePlain(c, std::move(d)), out);
+}
+
+int dpf_amd_pir_server_create_leader(const uint8_t* config, size_t config_len, dpf_amd_pir_db* db,
+                                     dpf_amd_pir_forward_fn forward, void* user,
+                                     dpf_amd_pir_server** out) {
+  PirConfig c;
+  std::unique_ptr<DenseDpfPirServer::Database> d;
+  int rc = PrepareServer(config, config_len, db, &c, &d);
+  if (rc != DPF_AMD_OK) return rc;
+  DpfPirServer::ForwardHelperRequestFn sender;
+  if (forward) {
+    sender = [forward, user](const PirRequest& helper_request,
+                             std::function<void()> while_waiting) -> StatusOr<PirResponse> {
+      const std::string req = helper_request.SerializeAsString();
+      dpf_amd_pir_call call;
+      call.while_waiting = &while_waiting;
+      int frc = forward(reinterpret_cast<const uint8_t*>(req.data()), req.size(), &call, user);
+      if (frc != DPF_AMD_OK) return CallbackStatus(frc, "ForwardHelperRequestFn");
+      if (!call.has_response)
+        return Status(StatusCode::kInternal, "ForwardHelperRequestFn returned no response");
+      PirResponse resp;
+      if (!resp.ParseFromArray(call.response.data(), call.response.size()))
+        return Status(StatusCode::kInternal, "malformed PirResponse from the Helper");
+      return resp;
+    };
+  }
+  return Finish(DenseDpfPirServer::CreateLeader(c, std::move(d), std::move(sender)), out);
+}
+
+int dpf_amd_pir_server_create_helper(const uint8_t* config, size_t config_len, dpf_amd_pir_db* db,
+                                     dpf_amd_pir_decrypt_fn decrypt, void* user,
+                                     dpf_amd_pir_server** out) {
+  PirConfig c;
+  std::unique_ptr<DenseDpfPirServer::Database> d;
+  int rc = PrepareServer(config, config_len, db, &c, &d);
+  if (rc != DPF_AMD_OK) return rc;
+  DpfPirServer::DecryptHelperRequestFn decrypter;
+  if (decrypt) {
+    decrypter = [decrypt, user](const std::string& ciphertext,
+                                const std::string& info) -> StatusOr<std::string> {
+      dpf_amd_pir_call call;
+      int drc = decrypt(reinterpret_cast<const uint8_t*>(ciphertext.data()), ciphertext.size(),
+                        reinterpret_cast<const uint8_t*>(info.data()), info.size(), &call, user);
+      if (drc != DPF_AMD_OK) return CallbackStatus(drc, "DecryptHelperRequestFn");
+      if (!call.has_response)
+        return Status(StatusCode::kInternal, "DecryptHelperRequestFn returned no plaintext");
+      return call.response;
+    };
+  }
+  return Finish(DenseDpfPirServer::CreateHelper(c, std::move(d), std::move(decrypter)), out);
 }
 
 void dpf_amd_pir_server_destroy(dpf_amd_pir_server* server) { delete server; }

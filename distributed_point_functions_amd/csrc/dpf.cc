@@ -676,7 +676,7 @@ class DeviceBuffer {
     return HipStatus(hipMemcpyAsync(p_, src, bytes, hipMemcpyHostToDevice, s), "upload");
   }
   void Reset() {
-    if (p_) hipFreeAsync(p_, stream_);
+    if (p_) (void)hipFreeAsync(p_, stream_);
     p_ = nullptr;
   }
   void* get() const { return p_; }

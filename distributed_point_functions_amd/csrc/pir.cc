@@ -135,7 +135,7 @@ StatusOr<std::unique_ptr<DenseDpfPirDatabase::Interface>> DenseDpfPirDatabase::B
 }
 
 DenseDpfPirDatabase::~DenseDpfPirDatabase() {
-  if (records_) hipFree(records_);
+  if (records_) (void)hipFree(records_);
 }
 
 StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductWithDevice(
@@ -154,8 +154,8 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductWithDevice(
                                          selection_blocks, num_queries, work, out, s));
   if (st.ok())
     st = HipStatus(hipMemcpyAsync(host.data(), out, host.size(), hipMemcpyDeviceToHost, s), "d2h");
-  hipFreeAsync(work, s);
-  if (out) hipFreeAsync(out, s);
+  (void)hipFreeAsync(work, s);
+  if (out) (void)hipFreeAsync(out, s);
   Status sync = HipStatus(hipStreamSynchronize(s), "sync");
   if (!st.ok()) return st;
   if (!sync.ok()) return sync;
@@ -196,8 +196,8 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductWith(
                                        hipMemcpyHostToDevice, s), "h2d");
   StatusOr<std::vector<std::string>> r =
       st.ok() ? InnerProductWithDevice(dev, blocks, q, s) : StatusOr<std::vector<std::string>>(st);
-  hipFreeAsync(dev, s);
-  hipStreamSynchronize(s);
+  (void)hipFreeAsync(dev, s);
+  (void)hipStreamSynchronize(s);
   return r;
 }
 
@@ -386,8 +386,8 @@ StatusOr<PirResponse> DenseDpfPirServer::HandlePlainRequest(const PirRequest& re
     StatusOr<std::vector<std::string>> r =
         st.ok() ? gpu_db->InnerProductWithDevice(sel, blocks, q, s)
                 : StatusOr<std::vector<std::string>>(st);
-    hipFreeAsync(sel, s);
-    hipStreamSynchronize(s);
+    (void)hipFreeAsync(sel, s);
+    (void)hipStreamSynchronize(s);
     if (!r.ok()) return r.status();
     inner_products = std::move(*r);
   } else {

@@ -288,6 +288,36 @@ int dpf_amd_pir_server_create_plain(const uint8_t* config, size_t config_len,
                                     dpf_amd_pir_db* db,
                                     dpf_amd_pir_server** out);
 void dpf_amd_pir_server_destroy(dpf_amd_pir_server* server);
+/* Leader / Helper roles (pir/dense_dpf_pir_server.h:65-82,
+ * pir/dpf_pir_server.cc:55-193). The reference's callbacks
+ * ForwardHelperRequestFn / DecryptHelperRequestFn (pir/dpf_pir_server.h:92-
+ * 109) become C function pointers that talk back through a call handle:
+ *   forward(helper_request, len, call, user): send the serialized PirRequest
+ *     to the Helper; while waiting for it call
+ *     dpf_amd_pir_call_while_waiting(call) (the Leader computes its own share
+ *     there), then hand the Helper's serialized PirResponse to
+ *     dpf_amd_pir_call_set_response(call, ...). Return 0, or a status code.
+ *   decrypt(ciphertext, len, context_info, info_len, call, user): decrypt the
+ *     EncryptedHelperRequest (Tink HybridDecrypt in the reference) and hand
+ *     the plaintext HelperRequest to dpf_amd_pir_call_set_response. */
+typedef struct dpf_amd_pir_call dpf_amd_pir_call;
+typedef int (*dpf_amd_pir_forward_fn)(const uint8_t* helper_request, size_t len,
+                                      dpf_amd_pir_call* call, void* user);
+typedef int (*dpf_amd_pir_decrypt_fn)(const uint8_t* ciphertext, size_t len,
+                                      const uint8_t* context_info,
+                                      size_t info_len, dpf_amd_pir_call* call,
+                                      void* user);
+int dpf_amd_pir_call_while_waiting(dpf_amd_pir_call* call);
+int dpf_amd_pir_call_set_response(dpf_amd_pir_call* call, const uint8_t* data,
+                                  size_t len);
+int dpf_amd_pir_server_create_leader(const uint8_t* config, size_t config_len,
+                                     dpf_amd_pir_db* db,
+                                     dpf_amd_pir_forward_fn forward, void* user,
+                                     dpf_amd_pir_server** out);
+int dpf_amd_pir_server_create_helper(const uint8_t* config, size_t config_len,
+                                     dpf_amd_pir_db* db,
+                                     dpf_amd_pir_decrypt_fn decrypt, void* user,
+                                     dpf_amd_pir_server** out);
 /* DpfPirServer::HandleRequest (pir/dpf_pir_server.h:123-124): serialized
  * PirRequest in, serialized PirResponse out. */
 int dpf_amd_pir_server_handle_request(const dpf_amd_pir_server* server,

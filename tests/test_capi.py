@@ -1,0 +1,52 @@
+"""The C-ABI library loads on a CPU-only machine and exports every function
+include/dpf_amd.h declares (no compute calls)."""
+import ctypes
+import os
+import re
+import subprocess
+
+from distributed_point_functions_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dpf_amd.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(dpf_amd_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    assert len(names) >= 40
+    for must in ("dpf_amd_evaluate_seeds", "dpf_amd_expand_and_correct",
+                 "dpf_amd_evaluate_points", "dpf_amd_inner_product",
+                 "dpf_amd_evaluate_until", "dpf_amd_pir_server_handle_request"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    missing = [n for n in declared_functions() if not hasattr(L, n)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (dpf_amd_\w+)", out))
+    assert set(declared_functions()) <= exported
+
+
+def test_version_and_error_plumbing():
+    L = _lib.lib()
+    assert L.dpf_amd_version().decode().startswith("dpf_amd")
+    # Tier-1 argument validation runs on the host before any HIP call.
+    rc = L.dpf_amd_evaluate_seeds(1, 3, 2, None, None, None, 0, None, None, None,
+                                  0, 0, 0, 0, None, None, None)
+    assert rc == 3
+    assert b"num_correction_words" in L.dpf_amd_last_error()
+
+
+def test_no_torch_types_in_the_abi():
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)  # code, not comments
+    for bad in ("torch", "at::", "c10", "std::", "Tensor"):
+        assert bad not in text

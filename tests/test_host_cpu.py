@@ -1,0 +1,217 @@
+"""Host logic of the product library on CPU (no kernel launches).
+
+  - key generation (host AES) reproduces the oracle's golden keys bit-exactly
+    and round-trips through the DpfKey wire format;
+  - validation errors carry the reference's status codes and messages
+    (dpf/distributed_point_function_test.cc:83-112, 160-190, 265-300,
+    510-650);
+  - value-type layout matches libstdc++ (tuple members reversed, naturally
+    aligned) and the hierarchy/tree bookkeeping (proto_validator.cc:113-158);
+  - without a GPU every evaluation entry point fails loudly (no CPU fallback).
+"""
+import json
+import os
+
+import pytest
+
+from distributed_point_functions_amd import value_types as V
+from distributed_point_functions_amd import wire
+from distributed_point_functions_amd._lib import DpfAmdError
+from distributed_point_functions_amd.dpf import (DistributedPointFunction, DpfKey, DpfParameters,
+                                                 decode_value)
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden.json")
+P32 = 4294967291
+P64 = 18446744073709551557
+
+
+def _spec(s):
+    if s[0] == "tuple":
+        return ("tuple", [_spec(c) for c in s[1]])
+    return tuple(s)
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+def _key_fields(dpf, k: DpfKey, levels):
+    return {"seed": k.seed, "party": k.party,
+            "cw_seeds": [c.seed for c in k.correction_words],
+            "ccl": [int(c.control_left) for c in k.correction_words],
+            "ccr": [int(c.control_right) for c in k.correction_words],
+            "value_corrections": _value_corrections(k, levels, dpf)}
+
+
+def _value_corrections(k, levels, dpf):
+    """Per hierarchy level, flattened value corrections (oracle order)."""
+    out = []
+    for h, (ld, spec, _) in enumerate(levels):
+        vt = V.from_spec(spec)
+        L = dpf.hierarchy_to_tree(h)
+        if h == len(levels) - 1:
+            vals = k.last_level_value_correction
+        else:
+            vals = k.correction_words[L].value_correction  # cc:131-148
+        out.append([x for v in vals for x in decode_value(vt, v)])
+    return out
+
+
+def test_product_keygen_matches_golden_keys(golden):
+    for case in golden["dpf"]:
+        levels = [(ld, _spec(s), sec) for ld, s, sec in case["levels"]]
+        params = [DpfParameters(ld, V.from_spec(s), sec) for ld, s, sec in levels]
+        dpf = DistributedPointFunction.create_incremental(params)
+        betas = [V.from_spec(l[1]).unflatten(iter(b)) for l, b in zip(levels, case["betas"])]
+        k0, k1 = dpf.generate_keys_incremental(case["alpha"], betas, seeds=case["seeds"])
+        for k, want in ((k0, case["key0"]), (k1, case["key1"])):
+            got = _key_fields(dpf, k, levels)
+            assert got["seed"] == want["seed"], case["name"]
+            assert got["party"] == want["party"]
+            assert got["cw_seeds"] == want["cw_seeds"], case["name"]
+            assert got["ccl"] == want["ccl"] and got["ccr"] == want["ccr"], case["name"]
+            assert got["value_corrections"] == want["value_corrections"], case["name"]
+            # wire round trip
+            assert DpfKey(bytes(k)) == k
+
+
+def test_random_keygen_differs_and_shares_structure():
+    dpf = DistributedPointFunction.create(DpfParameters(20, V.UINT64))
+    a0, a1 = dpf.generate_keys(5, 7)
+    b0, _ = dpf.generate_keys(5, 7)
+    assert a0.seed != b0.seed  # CSPRNG seeds
+    assert a0.party == 0 and a1.party == 1
+    assert len(a0.correction_words) == dpf.hierarchy_to_tree(0)
+    assert [c.seed for c in a0.correction_words] == [c.seed for c in a1.correction_words]
+
+
+@pytest.mark.parametrize("ld,spec,tree", [
+    (20, ("int", 64), 19), (20, ("int", 8), 16), (128, ("int", 128), 128),
+    (26, ("xor", 128), 26), (32, ("tuple", [("int", 32), ("intmodn", 64, P64)]), 32),
+    (0, ("int", 32), 0), (5, ("int", 32), 3)])
+def test_tree_levels(ld, spec, tree):
+    sec = 48 if "intmodn" in repr(spec) else 0.0
+    dpf = DistributedPointFunction.create(DpfParameters(ld, V.from_spec(spec), sec))
+    assert dpf.hierarchy_to_tree(0) == tree
+
+
+def test_c5_value_layout_and_descriptor():
+    vt = V.Tuple(V.Integer(32), V.IntModN(64, P64))
+    assert vt.size == 16 and vt.scalar_offsets() == [8, 0]
+    dpf = DistributedPointFunction.create(DpfParameters(32, vt, 48))
+    d = dpf.value_type_descriptor(0)
+    assert (d.num_scalars, d.blocks_needed, d.elements_per_block, d.out_stride) == (2, 2, 1, 16)
+    assert (d.scalars[0].out_offset, d.scalars[1].out_offset) == (8, 0)
+    assert d.scalars[1].modulus[0] == P64
+
+
+def test_tuple_layout_reverse_order():
+    vt = V.Tuple(V.Integer(8), V.Integer(16), V.Integer(32))
+    assert vt.size == 8 and vt.scalar_offsets() == [6, 4, 0]
+    vt = V.Tuple(V.Integer(64), V.Integer(8))
+    assert vt.size == 16 and vt.scalar_offsets() == [8, 0]
+
+
+# ----------------------------------------------------------- error messages
+def _err(fn):
+    with pytest.raises(DpfAmdError) as e:
+        fn()
+    return e.value
+
+
+def test_create_fails_for_tuple_with_different_intmodn():
+    e = _err(lambda: DistributedPointFunction.create(
+        DpfParameters(10, V.Tuple(V.IntModN(32, 3), V.IntModN(64, 4)))))
+    assert e.code == 12
+    assert e.message == "All elements of type IntModN in a tuple must be the same"
+
+
+def test_create_fails_for_invalid_value_type():
+    class Empty(V.ValueType):
+        def to_proto(self):
+            return b""
+    p = DpfParameters(10, Empty())
+    e = _err(lambda: DistributedPointFunction.create(p))
+    assert e.code == 3 and e.message.startswith("ValidateValueType: Unsupported ValueType")
+
+
+def test_create_fails_for_bad_log_domain_order():
+    e = _err(lambda: DistributedPointFunction.create_incremental(
+        [DpfParameters(10, V.UINT64), DpfParameters(10, V.UINT64)]))
+    assert e.code == 3
+    assert e.message == "`log_domain_size` fields must be in ascending order in `parameters`"
+
+
+def test_c5_default_security_parameter_rejected():
+    # int_mod_n.cc:29-67: 40 + 32 bits of security need more than the 66 bits
+    # a 64-bit modulus sample can provide.
+    e = _err(lambda: DistributedPointFunction.create(
+        DpfParameters(32, V.Tuple(V.Integer(32), V.IntModN(64, P64)))))
+    assert e.code == 3
+
+
+def test_generate_keys_errors():
+    dpf = DistributedPointFunction.create(DpfParameters(10, V.UINT32))
+    e = _err(lambda: dpf.generate_keys(1 << 10, 1))
+    assert e.code == 3 and e.message == "`alpha` must be smaller than the output domain size"
+    e = _err(lambda: dpf.generate_keys(0, 1 << 32))
+    assert e.code == 3
+    e = _err(lambda: dpf.generate_keys_incremental(0, [1, 2]))
+    assert e.code == 3
+    assert e.message == ("`beta` has to have the same size as `parameters` passed at "
+                         "construction")
+
+
+def test_evaluation_validation_errors_before_any_device_work():
+    params = [DpfParameters(5, V.UINT128), DpfParameters(10, V.UINT128)]
+    dpf = DistributedPointFunction.create_incremental(params)
+    k0, _ = dpf.generate_keys_incremental(3, [1, 2], seeds=(11, 12))
+    ctx = dpf.create_evaluation_context(k0)
+    e = _err(lambda: dpf.evaluate_until(-1, [], ctx))
+    assert e.message == "`hierarchy_level` must be non-negative and less than parameters_.size()"
+    e = _err(lambda: dpf.evaluate_until(2, [], ctx))
+    assert e.message == "`hierarchy_level` must be non-negative and less than parameters_.size()"
+    e = _err(lambda: dpf.evaluate_until(0, [0], ctx))
+    assert e.message == ("`prefixes` must be empty if and only if this is the first call with "
+                         "`ctx`.")
+    strange = V.Tuple(V.Integer(8), V.Integer(32), V.Integer(8), V.Integer(16), V.Integer(8))
+    e = _err(lambda: dpf.evaluate_until(0, [], ctx, value_type=strange))
+    assert e.message == "Value type T doesn't match parameters at `hierarchy_level`"
+
+
+def test_output_size_too_large():
+    params = [DpfParameters(10, V.UINT128), DpfParameters(100, V.UINT128)]
+    dpf = DistributedPointFunction.create_incremental(params)
+    k0, _ = dpf.generate_keys_incremental(123, [456, 789], seeds=(1, 2))
+    ctx = dpf.create_evaluation_context(k0)
+    e = _err(lambda: dpf.evaluate_until(1, [], ctx))
+    assert e.message == ("Output size would be larger than 2**62. Please evaluate fewer "
+                         "hierarchy levels at once.")
+
+
+def test_context_serialize_parse_round_trip():
+    params = [DpfParameters(5, V.UINT64), DpfParameters(12, V.UINT64)]
+    dpf = DistributedPointFunction.create_incremental(params)
+    k0, _ = dpf.generate_keys_incremental(17, [1, 2], seeds=(5, 6))
+    ctx = dpf.create_evaluation_context(k0)
+    data = ctx.serialize()
+    ctx2 = dpf.parse_evaluation_context(data)
+    assert ctx2.serialize() == data
+    assert ctx2.previous_hierarchy_level == -1
+    d = wire.decode(data)
+    assert DpfKey(d[2][-1]) == k0  # EvaluationContext.key (proto:156-171)
+
+
+def test_evaluation_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    dpf = DistributedPointFunction.create(DpfParameters(8, V.UINT64))
+    k0, _ = dpf.generate_keys(3, 4, seeds=(1, 2))
+    ctx = dpf.create_evaluation_context(k0)
+    e = _err(lambda: dpf.evaluate_next([], ctx))
+    assert e.code == 13  # INTERNAL: HIP error surfaced, no CPU fallback
+    e = _err(lambda: dpf.evaluate_at(k0, 0, [1, 2]))
+    assert e.code == 13
