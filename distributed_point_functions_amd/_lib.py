@@ -136,6 +136,10 @@ def _bind_tier2(L):
     _sig(L, "dpf_amd_pir_db_inner_product", I32, P, P, I64, I32, P)
     _sig(L, "dpf_amd_pir_server_create_plain", I32, P, SZ, P, PP)
     _sig(L, "dpf_amd_pir_server_destroy", None, P)
+    _sig(L, "dpf_amd_pir_call_while_waiting", I32, P)
+    _sig(L, "dpf_amd_pir_call_set_response", I32, P, P, SZ)
+    _sig(L, "dpf_amd_pir_server_create_leader", I32, P, SZ, P, P, P, PP)
+    _sig(L, "dpf_amd_pir_server_create_helper", I32, P, SZ, P, P, P, PP)
     _sig(L, "dpf_amd_pir_server_handle_request", I32, P, P, SZ, BUF,
          ctypes.POINTER(SZ))
 

@@ -1,0 +1,311 @@
+"""GPU parity of the reference's public API (Tier 2 of the C ABI): bit-exact
+against the committed golden fixtures and the CPU oracle.
+
+Follows the reference's tests:
+  - full-domain / EvaluateAt over value types: distributed_point_function_
+    test.cc:984-1079;
+  - incremental contexts (EvaluateNext on surviving prefixes, context state):
+    652-930;
+  - EvaluateAndApply vs per-level EvaluateAt: 1081-1142;
+  - dense PIR database inner product vs the unpacked definition:
+    pir/dense_dpf_pir_database_test.cc:274-326;
+  - PIR server plain / batched / concurrent: pir/dense_dpf_pir_server_test.cc:
+    288-366; Leader + Helper end to end with the one-time pad:
+    pir/dense_dpf_pir_client_test.cc:98-139, 230-244.
+"""
+import json
+import os
+import random
+import threading
+import zlib
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as po
+from tests.golden.make_golden import digest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden.json")
+
+
+def _spec(s):
+    if s[0] == "tuple":
+        return ("tuple", [_spec(c) for c in s[1]])
+    return tuple(s)
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def api(cuda):
+    from distributed_point_functions_amd import dpf, pir, value_types
+    return dpf, value_types, pir
+
+
+def _make(api, levels):
+    D, V, _ = api
+    params = [D.DpfParameters(ld, V.from_spec(s), sec) for ld, s, sec in levels]
+    return D.DistributedPointFunction.create_incremental(params)
+
+
+def test_golden_full_domain_and_evaluate_at(api, golden):
+    D, V, _ = api
+    for case in golden["dpf"]:
+        if len(case["levels"]) != 1:
+            continue
+        levels = [(ld, _spec(s), sec) for ld, s, sec in case["levels"]]
+        vt = V.from_spec(levels[0][1])
+        dpf = _make(api, levels)
+        beta = vt.unflatten(iter(case["betas"][0]))
+        k0, k1 = dpf.generate_keys(case["alpha"], beta, seeds=case["seeds"])
+        ev = case["eval"][0]
+        for k, want in ((k0, ev["digest0"]), (k1, ev["digest1"])):
+            got = vt.decode_flat(dpf.evaluate_next([], dpf.create_evaluation_context(k), raw=True))
+            assert len(got) == ev["count"]
+            assert digest(got) == want, case["name"]
+        e = case["evaluate_at"]
+        for k, want in ((k0, e["out0"]), (k1, e["out1"])):
+            got = vt.decode_flat(dpf.evaluate_at(k, 0, e["points"], raw=True))
+            assert got == want, case["name"]
+
+
+def test_golden_incremental_with_context_state(api, golden):
+    D, V, _ = api
+    case = next(c for c in golden["dpf"] if c["name"] == "incremental_u64")
+    levels = [(ld, _spec(s), sec) for ld, s, sec in case["levels"]]
+    dpf = _make(api, levels)
+    k0, k1 = dpf.generate_keys_incremental(case["alpha"], [b[0] for b in case["betas"]],
+                                           seeds=case["seeds"])
+    od = po.Dpf(levels)
+    ok0, ok1 = od.generate_keys(case["alpha"], [b[0] for b in case["betas"]],
+                                seeds=tuple(case["seeds"]))
+    for k, ok, dk in ((k0, ok0, "digest0"), (k1, ok1, "digest1")):
+        ctx = dpf.create_evaluation_context(k)
+        octx = od.create_evaluation_context(ok)
+        for ev in case["eval"]:
+            vt = V.from_spec(levels[ev["level"]][1])
+            got = vt.decode_flat(dpf.evaluate_next(ev["prefixes"], ctx, raw=True))
+            assert digest(got) == ev[dk]
+            od.evaluate_until(ev["level"], ev["prefixes"], octx)
+            assert ctx.previous_hierarchy_level == octx.previous_hierarchy_level
+            if ev["level"] + 1 < len(levels):
+                assert ctx.partial_evaluations_level == octx.partial_evaluations_level
+                assert sorted(ctx.partial_evaluations()) == sorted(
+                    (p, s, bool(c)) for p, s, c in octx.partial_evaluations())
+
+
+@pytest.mark.parametrize("spec", [("int", 64), ("int", 128), ("xor", 128),
+                                  ("tuple", [("int", 32), ("int", 32)])])
+def test_incremental_heavy_hitters_shape(api, spec):
+    """c3 in miniature: hierarchy every 8 bits, EvaluateNext on surviving
+    prefixes; bit-exact vs the oracle at every level, context serialised and
+    re-parsed between levels (resumable state)."""
+    lds = [8, 16, 24, 32]
+    levels = [(ld, spec, 40 + ld) for ld in lds]
+    rng = random.Random(zlib.crc32(repr(spec).encode()))
+    alpha = rng.getrandbits(32)
+    vt = api[1].from_spec(spec)
+    betas = [vt.unflatten(iter([rng.getrandbits(s[1]) for s in po.scalar_specs(spec)]))
+             for _ in lds]
+    seeds = (rng.getrandbits(128), rng.getrandbits(128))
+    dpf = _make(api, levels)
+    od = po.Dpf(levels)
+    k0, _ = dpf.generate_keys_incremental(alpha, betas, seeds=seeds)
+    ok0, _ = od.generate_keys(alpha, betas, seeds=seeds)
+    ctx = dpf.create_evaluation_context(k0)
+    octx = od.create_evaluation_context(ok0)
+    prefixes = []
+    for h, ld in enumerate(lds):
+        got = vt.decode_flat(dpf.evaluate_next(prefixes, ctx, raw=True))
+        want = od.evaluate_until(h, prefixes, octx)
+        assert got == want, h
+        ctx = dpf.parse_evaluation_context(ctx.serialize())
+        if h + 1 < len(lds):
+            prev = lds[h - 1] if h else 0
+            outs = [(p << (ld - prev)) | j for p in (prefixes or [0])
+                    for j in range(1 << (ld - prev))]
+            keep = set(rng.sample(outs, 64)) | {alpha >> (32 - ld)}
+            prefixes = sorted(keep)
+
+
+@pytest.mark.parametrize("lds", [[0, 1, 2], [8, 16, 32, 64], [0, 128], [128],
+                                 list(range(0, 129, 16))])
+def test_evaluate_and_apply_matches_per_level_evaluate_at(api, lds):
+    spec = ("int", 64)
+    levels = [(ld, spec, 40 + ld) for ld in lds]
+    top = (1 << lds[-1]) - 1
+    alpha = top
+    dpf = _make(api, levels)
+    od = po.Dpf(levels)
+    betas = [1000 + i for i in range(len(lds))]
+    k0, k1 = dpf.generate_keys_incremental(alpha, betas, seeds=(3, 4))
+    ok0, ok1 = od.generate_keys(alpha, betas, seeds=(3, 4))
+    points = [p & top for p in (23, 42, 123, 0, (1 << 128) - 1)]
+    keys, okeys = [k0, k1, k0, k1, k0], [ok0, ok1, ok0, ok1, ok0]
+    seen = []
+    dpf.evaluate_and_apply(keys, points, lambda vals: seen.append(list(vals)) or True)
+    assert len(seen) == len(lds)
+    for h, ld in enumerate(lds):
+        shift = lds[-1] - ld
+        for i, (ok, p) in enumerate(zip(okeys, points)):
+            prefix = p >> shift if shift < 128 else 0
+            assert seen[h][i] == od.evaluate_at(ok, h, [prefix])[0][0], (h, i)
+
+
+def test_evaluate_and_apply_stops_when_op_returns_false(api):
+    levels = [(8, ("int", 32), 48), (16, ("int", 32), 56)]
+    dpf = _make(api, levels)
+    k0, _ = dpf.generate_keys_incremental(5, [1, 2], seeds=(1, 2))
+    calls = []
+    dpf.evaluate_and_apply([k0], [5], lambda v: calls.append(v) and False)
+    assert len(calls) == 1
+
+
+# --------------------------------------------------------------------- PIR
+def _records(n, size, seed):
+    rng = np.random.default_rng(seed)
+    return [bytes(rng.integers(0, 256, size if size else rng.integers(0, 100),
+                               dtype=np.uint8)) for _ in range(n)]
+
+
+def test_pir_database_inner_product_golden(api, golden):
+    _, _, P = api
+    g = golden["pir"]
+    db = P.DenseDpfPirDatabase()
+    for r in g["records_hex"]:
+        db.insert(bytes.fromhex(r))
+    db.build()
+    assert db.size == len(g["records_hex"])
+    assert [o.hex() for o in db.inner_product_with(g["selections"])] == g["out_hex"]
+
+
+@pytest.mark.parametrize("n,size", [(1, 16), (127, 80), (128, 81), (1000, 256), (4099, 17)])
+def test_pir_database_inner_product_vs_oracle(api, n, size):
+    _, _, P = api
+    records = _records(n, size, n)
+    rng = random.Random(n)
+    sels = [[rng.getrandbits(128) for _ in range((n + 127) // 128)] for _ in range(3)]
+    db = P.DenseDpfPirDatabase()
+    db.insert_fixed(np.frombuffer(b"".join(records), np.uint8).reshape(n, size))
+    db.build()
+    assert db.inner_product_with(sels) == po.inner_product(records, sels)
+
+
+def _pir_setup(api, n, size, seed=0):
+    D, V, P = api
+    records = _records(n, size, seed)
+    ld = max(0, (n - 1).bit_length())
+    dpf = D.DistributedPointFunction.create(D.DpfParameters(ld, V.XorWrapper(128)))
+    return records, dpf
+
+
+def _plain_server(api, records):
+    _, _, P = api
+    db = P.DenseDpfPirDatabase()
+    for r in records:
+        db.insert(r)
+    return P.DenseDpfPirServer.create_plain(len(records), db)
+
+
+def test_pir_plain_server_matches_oracle_and_reconstructs(api):
+    _, _, P = api
+    n = 1000
+    records, dpf = _pir_setup(api, n, 48)
+    server = _plain_server(api, records)
+    idx = [0, 5, 500, 999, 128, 127]
+    pairs = P.client_keys(dpf, n, idx, seeds=[(2 * i + 1, 2 * i + 2) for i in range(len(idx))])
+    r0 = P.parse_response(server.handle_request(P.pir_request_plain([a for a, _ in pairs])))
+    r1 = P.parse_response(server.handle_request(P.pir_request_plain([b for _, b in pairs])))
+    for i, a, b in zip(idx, r0, r1):
+        assert bytes(x ^ y for x, y in zip(a, b)) == records[i]
+    # response of one server == oracle inner product with the oracle's expansion
+    ld = max(0, (n - 1).bit_length())
+    od = po.Dpf([(ld, ("xor", 128), 40 + ld)])
+    nb = (n + 127) // 128
+    for j, i in enumerate(idx):
+        ok0, _ = od.generate_keys(i // 128, [1 << (i % 128)], seeds=(2 * j + 1, 2 * j + 2))
+        sel = [v[0] for v in od.evaluate_until(0, [], od.create_evaluation_context(ok0))[:nb]]
+        assert r0[j] == po.inner_product(records, [sel])[0]
+
+
+def test_pir_batched_equals_singles_and_concurrent(api):
+    _, _, P = api
+    n = 777
+    records, dpf = _pir_setup(api, n, 33, seed=3)
+    server = _plain_server(api, records)
+    idx = list(range(0, n, 97))
+    keys = [a for a, _ in P.client_keys(dpf, n, idx)]
+    batched = P.parse_response(server.handle_request(P.pir_request_plain(keys)))
+    singles = [P.parse_response(server.handle_request(P.pir_request_plain([k])))[0]
+               for k in keys]
+    assert batched == singles
+    results, errors = [None] * 16, []
+
+    def worker(t):
+        try:
+            results[t] = P.parse_response(server.handle_request(P.pir_request_plain(keys)))
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors and all(r == batched for r in results)
+
+
+def test_pir_leader_helper_end_to_end_with_one_time_pad(api):
+    _, _, P = api
+    n = 3000
+    records, dpf = _pir_setup(api, n, 64, seed=7)
+    idx = [2, 1500, 2999]
+    pairs = P.client_keys(dpf, n, idx)
+    otp_seed = bytes(range(16))
+    helper_req = P.helper_request([b for _, b in pairs], otp_seed)
+    encrypted = b"ct:" + helper_req  # stand-in for Tink HybridEncrypt
+
+    def decrypter(ct, info):
+        assert info == P.DenseDpfPirServer.ENCRYPTION_CONTEXT_INFO
+        return ct[3:]
+
+    def mk_db():
+        db = P.DenseDpfPirDatabase()
+        for r in records:
+            db.insert(r)
+        return db
+    helper = P.DenseDpfPirServer.create_helper(n, mk_db(), decrypter)
+
+    def sender(req, while_waiting):
+        while_waiting()
+        return helper.handle_request(req)
+    leader = P.DenseDpfPirServer.create_leader(n, mk_db(), sender)
+    resp = P.parse_response(leader.handle_request(
+        P.pir_request_leader([a for a, _ in pairs], encrypted)))
+    pad = po.aes_ctr_prng(otp_seed, sum(len(r) for r in resp))
+    off = 0
+    for i, r in zip(idx, resp):
+        assert bytes(x ^ y for x, y in zip(r, pad[off:off + len(r)])) == records[i]
+        off += len(r)
+
+
+def test_pir_leader_requires_while_waiting(api):
+    from distributed_point_functions_amd._lib import DpfAmdError
+    _, _, P = api
+    n = 200
+    records, dpf = _pir_setup(api, n, 16)
+    db = P.DenseDpfPirDatabase()
+    for r in records:
+        db.insert(r)
+    leader = P.DenseDpfPirServer.create_leader(n, db, lambda req, ww: b"")
+    (a, _), = P.client_keys(dpf, n, [3])
+    with pytest.raises(DpfAmdError) as e:
+        leader.handle_request(P.pir_request_leader([a], b"x"))
+    assert e.value.code == 9
+    assert e.value.message == ("HandleRequest: `while_waiting` was not called from `sender` "
+                               "passed at construction.")
