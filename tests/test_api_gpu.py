@@ -138,7 +138,7 @@ def test_incremental_heavy_hitters_shape(api, spec):
                                  list(range(0, 129, 16))])
 def test_evaluate_and_apply_matches_per_level_evaluate_at(api, lds):
     spec = ("int", 64)
-    levels = [(ld, spec, 40 + ld) for ld in lds]
+    levels = [(ld, spec, 0) for ld in lds]  # default security_parameter
     top = (1 << lds[-1]) - 1
     alpha = top
     dpf = _make(api, levels)
