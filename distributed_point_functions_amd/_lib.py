@@ -10,7 +10,9 @@ import ctypes
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "_native", "libdpf_amd.so")
+# DPF_AMD_LIB selects another in-tree build of the same library (kernel
+# variants built by tools/build_variants.py for A/B measurements).
+LIB_PATH = os.environ.get("DPF_AMD_LIB") or os.path.join(PKG, "_native", "libdpf_amd.so")
 
 MAX_SCALARS = 16
 MAX_CORRECTIONS = 32

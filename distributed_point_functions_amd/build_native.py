@@ -25,8 +25,9 @@ CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
 
 
 def _sources():
-    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) +
-                  glob.glob(os.path.join(CSRC, "*.cc")))
+    # largest device translation units first so the parallel build ends early
+    srcs = glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cc"))
+    return sorted(srcs, key=lambda s: ("k_expand" not in s, not s.endswith(".hip"), s))
 
 
 def _headers_mtime():
@@ -36,12 +37,12 @@ def _headers_mtime():
     return max([os.path.getmtime(h) for h in hs] + [0])
 
 
-def _compile(src: str, force: bool) -> str:
-    obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+def _compile(src: str, force: bool, obj_dir: str = OBJ_DIR, defines=()) -> str:
+    obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
     if (not force and os.path.exists(obj) and
             os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime())):
         return obj
-    cmd = ["hipcc"] + CXXFLAGS + ["-c", src, "-o", obj + ".tmp"]
+    cmd = ["hipcc"] + CXXFLAGS + ["-D" + d for d in defines] + ["-c", src, "-o", obj + ".tmp"]
     if src.endswith(".hip"):
         cmd[1:1] = ["--offload-arch=" + ARCH, "-x", "hip"]
     else:

@@ -1,0 +1,461 @@
+// aes_device.h — device building blocks shared by the gfx950 kernels: the
+// LDS T-table AES core, the DPF PRG steps and the value conversion/correction.
+//
+// AES design: CDNA4 has no AES instructions, so AES-128 runs
+// as T-table lookups from LDS.  One 64 KiB table per workgroup holds, for each
+// of the 256 byte values e, a 256-byte row [T0[e] x 32 | T1[e] x 32]: lane l
+// reads replica (l & 31), i.e. bank (l & 31), so every ds_read_b32 is
+// bank-conflict free whatever the data.  The row address is built with ONE
+// v_perm_b32 (state byte -> address bits 8..15, lane offset -> bits 0..7);
+// T1 is the same address + 128 (ds_read offset field), T2/T3 are rotations
+// of T0/T1 folded into one v_alignbit per column.  Per round and column:
+// 4 v_perm + 4 ds_read_b32 + 3 VALU; the round keys are SGPR constants.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "aes_tables.h"
+#include "dpf_amd.h"
+#include "internal.h"
+#include "kernel_args.h"
+
+namespace dpf_amd {
+
+// One copy per translation unit (each .hip file is its own code object).
+static __constant__ Te0Table c_te0 = MakeTe0();
+
+// ----------------------------------------------------------------------------
+// AES core
+// ----------------------------------------------------------------------------
+
+struct Lds {
+  const char* base;
+  uint32_t laneoff;
+};
+
+__device__ __forceinline__ void FillTables(uint32_t* tab) {
+  for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) {
+    uint32_t v = c_te0.t[i >> 6];
+    tab[i] = (i & 32) ? ((v << 8) | (v >> 24)) : v;  // T1 = rotl8(T0)
+  }
+}
+
+__device__ __forceinline__ Lds MakeLds(const uint32_t* tab) {
+  return Lds{reinterpret_cast<const char*>(tab), (threadIdx.x & 31u) * 4u};
+}
+
+// Byte k of x to address bits 8..15, lane offset to bits 0..7.
+#define DPF_SEL(k) (0x0c0c0000u | ((4u + (k)) << 8))
+
+__device__ __forceinline__ uint32_t LoadT0(const Lds& L, uint32_t x, int k) {
+  uint32_t a = __builtin_amdgcn_perm(x, L.laneoff, DPF_SEL(k));
+  return *reinterpret_cast<const uint32_t*>(L.base + a);
+}
+__device__ __forceinline__ uint32_t LoadT1(const Lds& L, uint32_t x, int k) {
+  uint32_t a = __builtin_amdgcn_perm(x, L.laneoff, DPF_SEL(k));
+  return *reinterpret_cast<const uint32_t*>(L.base + a + 128);
+}
+__device__ __forceinline__ uint32_t Rotl16(uint32_t x) {
+  return __builtin_amdgcn_alignbit(x, x, 16);
+}
+
+__device__ __forceinline__ uint32_t Xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // one v_bitop3_b32
+}
+
+// The three DPF PRG keys (cc:55-60) expanded at compile time.  Device code
+// indexes them with unrolled constant indices, so every round-key word is a
+// literal materialised by s_mov (SALU) next to its use: no constant-memory
+// loads, no SGPR pressure, no VGPR-lane spills of hoisted keys.
+constexpr AesKey kDpfKeys[3] = {ExpandAesKey(kPrgKeyLeftLo, kPrgKeyLeftHi),
+                                ExpandAesKey(kPrgKeyRightLo, kPrgKeyRightHi),
+                                ExpandAesKey(kPrgKeyValueLo, kPrgKeyValueHi)};
+
+// Key accessors: rk(n, i) / rkr(n, i) for state n, round-key word i.
+template <int W>
+struct DpfKeyAt {  // one fixed DPF key for all states
+  __device__ __forceinline__ uint32_t rk(int, int i) const { return kDpfKeys[W].rk[i]; }
+  __device__ __forceinline__ uint32_t rkr(int, int i) const { return kDpfKeys[W].rkr[i]; }
+};
+struct DpfLeftRight {  // state 0: left key, state 1: right key
+  __device__ __forceinline__ uint32_t rk(int n, int i) const { return kDpfKeys[n].rk[i]; }
+  __device__ __forceinline__ uint32_t rkr(int n, int i) const { return kDpfKeys[n].rkr[i]; }
+};
+struct DpfSelect {  // per-lane choice of the left / right key (path walk)
+  bool right;
+  __device__ __forceinline__ uint32_t rk(int, int i) const {
+    return right ? kDpfKeys[1].rk[i] : kDpfKeys[0].rk[i];
+  }
+  __device__ __forceinline__ uint32_t rkr(int, int i) const {
+    return right ? kDpfKeys[1].rkr[i] : kDpfKeys[0].rkr[i];
+  }
+};
+struct PairSelect {  // generic keys from a kernel argument
+  const KeyPair& kp;
+  bool right;
+  __device__ __forceinline__ uint32_t rk(int, int i) const {
+    return right ? kp.k[1].rk[i] : kp.k[0].rk[i];
+  }
+  __device__ __forceinline__ uint32_t rkr(int, int i) const {
+    return right ? kp.k[1].rkr[i] : kp.k[0].rkr[i];
+  }
+};
+
+// N independent AES-128 encryptions in lockstep.  Each round first forms all
+// 16N table addresses (v_perm), then issues all 16N ds_read_b32 back to back
+// (sched_group_barrier keeps the scheduler from splitting them into small
+// waitcnt-separated groups), then combines: per output column
+// T0[a] ^ T1[b] ^ rotl16(T0[c] ^ T1[d] ^ rotr16(rk)) = 2 v_bitop3 + 1 alignbit.
+template <int N, class K>
+__device__ __forceinline__ void AesN(uint32_t (&w)[N][4], const K& key,
+                                     const Lds& L) {
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[n][c] ^= key.rk(n, c);
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    uint32_t t[N][4][4];
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        t[n][c][0] = LoadT0(L, w[n][c], 0);
+        t[n][c][1] = LoadT1(L, w[n][(c + 1) & 3], 1);
+        t[n][c][2] = LoadT0(L, w[n][(c + 2) & 3], 2);
+        t[n][c][3] = LoadT1(L, w[n][(c + 3) & 3], 3);
+      }
+    __builtin_amdgcn_sched_group_barrier(0x002, 16 * N, 0);  // address VALU
+    __builtin_amdgcn_sched_group_barrier(0x100, 16 * N, 0);  // DS reads
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        w[n][c] = Xor3(t[n][c][0], t[n][c][1],
+                       Rotl16(Xor3(t[n][c][2], t[n][c][3], key.rkr(n, 4 * r + c))));
+  }
+  // Last round: S-box bytes are byte 1/2 of T0 and byte 3 of T1.
+  uint32_t t[N][4][4];
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      t[n][c][0] = LoadT0(L, w[n][c], 0);
+      t[n][c][1] = LoadT0(L, w[n][(c + 1) & 3], 1);
+      t[n][c][2] = LoadT0(L, w[n][(c + 2) & 3], 2);
+      t[n][c][3] = LoadT1(L, w[n][(c + 3) & 3], 3);
+    }
+  __builtin_amdgcn_sched_group_barrier(0x002, 16 * N, 0);
+  __builtin_amdgcn_sched_group_barrier(0x100, 16 * N, 0);
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t lo = __builtin_amdgcn_perm(t[n][c][1], t[n][c][0], 0x0c0c0501u);
+      const uint32_t hi = __builtin_amdgcn_perm(t[n][c][3], t[n][c][2], 0x07020c0cu);
+      w[n][c] = Xor3(lo, hi, key.rk(n, 40 + c));
+    }
+}
+
+// sigma(x) = (x.hi ^ x.lo, x.hi) (aes_128_fixed_key_hash.cc:75-78) in words.
+__device__ __forceinline__ void Sigma(const uint32_t (&x)[4], uint32_t (&s)[4]) {
+  s[0] = x[2];
+  s[1] = x[3];
+  s[2] = x[0] ^ x[2];
+  s[3] = x[1] ^ x[3];
+}
+
+__device__ __forceinline__ u128 ToU128(const uint32_t (&x)[4]) {
+  return (u128)x[0] | ((u128)x[1] << 32) | ((u128)x[2] << 64) | ((u128)x[3] << 96);
+}
+__device__ __forceinline__ void FromU128(u128 v, uint32_t (&x)[4]) {
+  x[0] = (uint32_t)v;
+  x[1] = (uint32_t)(v >> 32);
+  x[2] = (uint32_t)(v >> 64);
+  x[3] = (uint32_t)(v >> 96);
+}
+
+// ----------------------------------------------------------------------------
+// Value conversion + correction (vth:216-328, 447-460, 507-515, 586-606;
+// int_mod_n.h:121-250; h:852-858)
+// ----------------------------------------------------------------------------
+
+__device__ __forceinline__ u128 MaskBytes(int nbytes) {
+  return nbytes >= 16 ? ~(u128)0 : (((u128)1 << (8 * nbytes)) - 1);
+}
+
+template <int BN>
+__device__ __forceinline__ u128 PickWord(const u128 (&W)[BN], int j) {
+  u128 r = W[0];
+#pragma unroll
+  for (int i = 1; i < BN; ++i)
+    if (j == i) r = W[i];
+  return r;
+}
+
+// Little-endian bytes [off, off + nbytes) of the hashed blocks.
+template <int BN>
+__device__ __forceinline__ u128 GetBytes(const u128 (&W)[BN], int off, int nbytes) {
+  int j = off >> 4;
+  int sh = (off & 15) * 8;
+  u128 v = PickWord<BN>(W, j) >> sh;
+  if (sh != 0 && j + 1 < BN) v |= PickWord<BN>(W, j + 1) << (128 - sh);
+  return v & MaskBytes(nbytes);
+}
+
+__device__ __forceinline__ u128 ScAdd(const ScalarDev& s, u128 a, u128 b) {
+  if (s.kind == DPF_AMD_KIND_INTEGER) return (a + b) & MaskBytes(s.bytes);
+  if (s.kind == DPF_AMD_KIND_XOR_WRAPPER) return a ^ b;
+  u128 x = s.mod - b;  // IntModN AddBaseInteger (int_mod_n.h:213-223)
+  return a >= x ? a - x : s.mod - x + a;
+}
+
+__device__ __forceinline__ u128 ScNeg(const ScalarDev& s, u128 a) {
+  if (s.kind == DPF_AMD_KIND_INTEGER) return (0 - a) & MaskBytes(s.bytes);
+  if (s.kind == DPF_AMD_KIND_XOR_WRAPPER) return a;
+  return a == 0 ? (u128)0 : s.mod - a;
+}
+
+// block -> (block / m, block % m).  Pseudo-Mersenne moduli m = 2^w - c with
+// small c fold the high part (2^w = c mod m); others use 128-bit division.
+__device__ __forceinline__ void DivMod(const ScalarDev& s, u128 x, u128& q, u128& r) {
+  if (s.use_fold) {
+    const int w = s.fold_w;
+    const u128 low = ((u128)1 << w) - 1;
+    u128 qq = 0;
+    while ((x >> w) != 0) {
+      u128 hi = x >> w;
+      qq += hi;
+      x = hi * s.fold_c + (x & low);
+    }
+    if (x >= s.mod) {
+      x -= s.mod;
+      qq += 1;
+    }
+    q = qq;
+    r = x;
+  } else {
+    q = x / s.mod;
+    r = x % s.mod;
+  }
+}
+
+__device__ __forceinline__ void StoreScalar(char* p, int nbytes, u128 v) {
+  switch (nbytes) {
+    case 1:
+      *reinterpret_cast<uint8_t*>(p) = (uint8_t)v;
+      break;
+    case 2:
+      *reinterpret_cast<uint16_t*>(p) = (uint16_t)v;
+      break;
+    case 4:
+      *reinterpret_cast<uint32_t*>(p) = (uint32_t)v;
+      break;
+    case 8:
+      *reinterpret_cast<uint64_t*>(p) = (uint64_t)v;
+      break;
+    default: {
+      uint4 u;
+      u.x = (uint32_t)v;
+      u.y = (uint32_t)(v >> 32);
+      u.z = (uint32_t)(v >> 64);
+      u.w = (uint32_t)(v >> 96);
+      *reinterpret_cast<uint4*>(p) = u;
+    }
+  }
+}
+
+__device__ __forceinline__ u128 Correct(const ScalarDev& s, u128 v, bool t,
+                                        u128 corr, int party) {
+  if (t) v = ScAdd(s, v, corr);
+  if (party == 1) v = ScNeg(s, v);
+  return v;
+}
+
+// Converts the hashed blocks of one tree leaf and writes elements
+// [e_begin, e_end) (ConvertBytesToArrayOf + correction, h:846-862).
+// `corr` points at the correction of element 0; `elem_out(e)` gives the
+// destination of element e.
+template <int BN, class Out>
+__device__ __forceinline__ void EmitLeaf(const VtDev& vt, const u128 (&W)[BN],
+                                         bool t, int party, const u128* corr,
+                                         int e_begin, int e_end, Out elem_out) {
+  if (vt.direct) {
+    for (int e = e_begin; e < e_end; ++e) {
+      char* dst = elem_out(e);
+      for (int s = 0; s < vt.ns; ++s) {
+        const ScalarDev& sc = vt.sc[s];
+        u128 v = GetBytes<BN>(W, e * vt.esz + sc.in_off, sc.bytes);
+        v = Correct(sc, v, t, corr[e * vt.ns + s], party);
+        StoreScalar(dst + sc.out_off, sc.bytes, v);
+      }
+    }
+    return;
+  }
+  // Sampling path (an IntModN is present; epb == 1).
+  char* dst = elem_out(0);
+  u128 block = W[0];
+  int pos = 16;
+  for (int s = 0; s < vt.ns; ++s) {
+    const ScalarDev& sc = vt.sc[s];
+    const bool update = s + 1 < vt.ns;
+    u128 v;
+    if (sc.kind == DPF_AMD_KIND_INT_MOD_N) {
+      u128 q, r;
+      DivMod(sc, block, q, r);
+      v = r;
+      if (update) {
+        block = (sc.bytes < 16) ? (q << (8 * sc.bytes)) : (u128)0;
+        block |= GetBytes<BN>(W, pos, sc.bytes);
+        pos += sc.bytes;
+      }
+    } else {
+      v = block & MaskBytes(sc.bytes);
+      if (update) {
+        block = (sc.bytes < 16) ? (block & ~MaskBytes(sc.bytes)) : (u128)0;
+        block |= GetBytes<BN>(W, pos, sc.bytes);
+        pos += sc.bytes;
+      }
+    }
+    v = Correct(sc, v, t, corr[s], party);
+    StoreScalar(dst + sc.out_off, sc.bytes, v);
+  }
+}
+
+// Value PRG of NS seeds: block j of seed n = H_value(seed_n + j)
+// (HashExpandedSeeds, cc:523-547).
+template <int NS, int BN>
+__device__ __forceinline__ void HashSeeds(const uint32_t (&x)[NS][4], u128 (&W)[NS][BN],
+                                          const Lds& L) {
+  uint32_t st[NS * BN][4], sg[NS * BN][4];
+#pragma unroll
+  for (int n = 0; n < NS; ++n) {
+    u128 base = ToU128(x[n]);
+#pragma unroll
+    for (int j = 0; j < BN; ++j) {
+      uint32_t y[4];
+      FromU128(base + (u128)j, y);
+      Sigma(y, sg[n * BN + j]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) st[n * BN + j][c] = sg[n * BN + j][c];
+    }
+  }
+  AesN<NS * BN>(st, DpfKeyAt<2>{}, L);
+#pragma unroll
+  for (int i = 0; i < NS * BN; ++i) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) st[i][c] ^= sg[i][c];
+  }
+#pragma unroll
+  for (int n = 0; n < NS; ++n)
+#pragma unroll
+    for (int j = 0; j < BN; ++j) W[n][j] = ToU128(st[n * BN + j]);
+}
+
+// ----------------------------------------------------------------------------
+// Tree steps (ExpandSeeds cc:327-370; EvaluateSeeds evaluate_prg_hwy.cc:
+// 552-634).  Seed correction is applied before the control bit is extracted.
+// ----------------------------------------------------------------------------
+
+struct Cw {
+  uint32_t seed[4];
+  uint32_t cl, cr;
+};
+
+__device__ __forceinline__ Cw LoadCw(const uint4* cw_seed, const uint8_t* ccl,
+                                     const uint8_t* ccr, int64_t i) {
+  uint4 s = cw_seed[i];
+  Cw c;
+  c.seed[0] = s.x;
+  c.seed[1] = s.y;
+  c.seed[2] = s.z;
+  c.seed[3] = s.w;
+  c.cl = ccl[i];
+  c.cr = ccr[i];
+  return c;
+}
+
+// Both children of x (left at 2j, right at 2j+1).
+__device__ __forceinline__ void Expand2(const uint32_t (&x)[4], uint32_t t, const Cw& cw,
+                                        const Lds& L, uint32_t (&l)[4], uint32_t& tl,
+                                        uint32_t (&r)[4], uint32_t& tr) {
+  uint32_t s[4], st[2][4];
+  Sigma(x, s);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) st[0][c] = st[1][c] = s[c];
+  AesN<2>(st, DpfLeftRight{}, L);
+  const uint32_t m = 0u - t;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    l[c] = st[0][c] ^ s[c] ^ (cw.seed[c] & m);
+    r[c] = st[1][c] ^ s[c] ^ (cw.seed[c] & m);
+  }
+  tl = (l[0] & 1u) ^ (t & cw.cl);
+  tr = (r[0] & 1u) ^ (t & cw.cr);
+  l[0] &= ~1u;
+  r[0] &= ~1u;
+}
+
+// One path step with the key chosen by `bit` (per lane).
+template <class K>
+__device__ __forceinline__ void WalkStep(uint32_t (&x)[4], uint32_t& t, uint32_t bit,
+                                         const Cw& cw, const K& key, const Lds& L) {
+  uint32_t s[4], st[1][4];
+  Sigma(x, s);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) st[0][c] = s[c];
+  AesN<1>(st, key, L);
+  const uint32_t m = 0u - t;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) x[c] = st[0][c] ^ s[c] ^ (cw.seed[c] & m);
+  uint32_t nt = (x[0] & 1u) ^ (t & (bit ? cw.cr : cw.cl));
+  x[0] &= ~1u;
+  t = nt;
+}
+
+// ----------------------------------------------------------------------------
+// Leaf emitters: value conversion + correction + store of one tree leaf.
+// EmitGeneric handles every supported T through the runtime descriptor; the
+// specialised emitters cover the benchmark types without 128-bit generic code
+// (they produce bit-identical results; tests compare both against the oracle).
+// ----------------------------------------------------------------------------
+
+struct ExpandCtx {
+  const ExpandArgs& a;
+  const VtDev& vt;
+  const Lds& L;
+};
+
+// Value PRG of one seed: block j = H_value(seed + j) (cc:523-547).
+template <int NS, int BN>
+__device__ __forceinline__ void HashWords(const uint32_t (&x)[NS][4],
+                                          uint32_t (&h)[NS][BN][4], const Lds& L) {
+  uint32_t st[NS * BN][4], sg[NS * BN][4];
+#pragma unroll
+  for (int n = 0; n < NS; ++n) {
+#pragma unroll
+    for (int j = 0; j < BN; ++j) {
+      uint32_t y[4];
+      if (j == 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) y[c] = x[n][c];
+      } else {
+        FromU128(ToU128(x[n]) + (u128)j, y);
+      }
+      Sigma(y, sg[n * BN + j]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) st[n * BN + j][c] = sg[n * BN + j][c];
+    }
+  }
+  AesN<NS * BN>(st, DpfKeyAt<2>{}, L);
+#pragma unroll
+  for (int n = 0; n < NS; ++n)
+#pragma unroll
+    for (int j = 0; j < BN; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) h[n][j][c] = st[n * BN + j][c] ^ sg[n * BN + j][c];
+}
+
+}  // namespace dpf_amd

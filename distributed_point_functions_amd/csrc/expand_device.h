@@ -1,0 +1,238 @@
+// expand_device.h — the fused subtree-expansion kernel KExpand<D, Emitter>
+// (ExpandSeeds cc:289-372 + HashExpandedSeeds cc:523-547 + the correction loop
+// of EvaluateUntil h:836-862) and its leaf emitters.  Included by the
+// k_expand_*.hip translation units, each instantiating a few emitters.
+#pragma once
+
+#include "aes_device.h"
+
+namespace dpf_amd {
+
+template <int BN>
+struct EmitGeneric {
+  static constexpr int kBN = BN;
+  __device__ static void Emit(const ExpandCtx& E, const uint32_t (&h)[BN][4], uint32_t t,
+                              int64_t g) {
+    const VtDev& vt = E.vt;
+    if (g < E.a.leaf_begin || g >= E.a.leaf_end) return;
+    u128 W[BN];
+#pragma unroll
+    for (int j = 0; j < BN; ++j) W[j] = ToU128(h[j]);
+    char* base = E.a.out + (g - E.a.leaf_begin) * (int64_t)vt.cepb * vt.stride;
+    const int stride = vt.stride;
+    EmitLeaf<BN>(vt, W, t != 0, vt.party, vt.corr, 0, vt.cepb,
+                 [base, stride](int e) { return base + (int64_t)e * stride; });
+  }
+};
+
+// Lane-wise (SWAR) arithmetic on a 16-byte block of B-byte integers.
+template <int B>
+__device__ __forceinline__ void SwarAdd(uint32_t (&a)[4], const uint32_t (&b)[4]) {
+  if constexpr (B == 16) {
+    FromU128(ToU128(a) + ToU128(b), a);
+  } else if constexpr (B == 8) {
+#pragma unroll
+    for (int i = 0; i < 4; i += 2) {
+      uint64_t x = ((uint64_t)a[i + 1] << 32 | a[i]) + ((uint64_t)b[i + 1] << 32 | b[i]);
+      a[i] = (uint32_t)x;
+      a[i + 1] = (uint32_t)(x >> 32);
+    }
+  } else if constexpr (B == 4) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] += b[i];
+  } else {
+    constexpr uint32_t H = (B == 2) ? 0x80008000u : 0x80808080u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = ((a[i] & ~H) + (b[i] & ~H)) ^ ((a[i] ^ b[i]) & H);
+  }
+}
+
+template <int B>
+__device__ __forceinline__ void SwarNeg(uint32_t (&a)[4]) {
+  if constexpr (B == 16) {
+    FromU128((u128)0 - ToU128(a), a);
+  } else if constexpr (B == 8) {
+#pragma unroll
+    for (int i = 0; i < 4; i += 2) {
+      uint64_t x = 0 - ((uint64_t)a[i + 1] << 32 | a[i]);
+      a[i] = (uint32_t)x;
+      a[i + 1] = (uint32_t)(x >> 32);
+    }
+  } else if constexpr (B == 4) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = 0u - a[i];
+  } else {
+    constexpr uint32_t one = (B == 2) ? 0x00010001u : 0x01010101u;
+    uint32_t o[4] = {one, one, one, one};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = ~a[i];
+    SwarAdd<B>(a, o);
+  }
+}
+
+// T is a single directly-convertible B-byte integer or XorWrapper
+// (uint8..uint128, XorWrapper<uint8..uint128>): the elements of a leaf are the
+// consecutive B-byte slices of the hashed block (vth:586-598).
+template <int B>
+struct EmitDirect {
+  static constexpr int kBN = 1;
+  __device__ static void Emit(const ExpandCtx& E, const uint32_t (&h)[1][4], uint32_t t,
+                              int64_t g) {
+    const VtDev& vt = E.vt;
+    if (g < E.a.leaf_begin || g >= E.a.leaf_end) return;
+    uint32_t w[4], c[4];
+    const uint32_t m = 0u - t;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      w[i] = h[0][i];
+      c[i] = (uint32_t)(vt.corr_packed >> (32 * i)) & m;
+    }
+    if (vt.sc[0].kind == DPF_AMD_KIND_XOR_WRAPPER) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w[i] ^= c[i];
+    } else {
+      SwarAdd<B>(w, c);
+      if (vt.party == 1) SwarNeg<B>(w);
+    }
+    char* dst = E.a.out + (g - E.a.leaf_begin) * (int64_t)vt.cepb * B;
+    if (vt.cepb * B == 16) {
+      *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      const u128 v = ToU128(w);
+      for (int e = 0; e < vt.cepb; ++e) StoreScalar(dst + e * B, B, v >> (8 * B * e));
+    }
+  }
+};
+
+// T = Tuple<uint32_t, IntModN<uint64_t, m>> with m = 2^64 - c, c < 2^56
+// (the c5 benchmark type).  Sampling path of vth:230-251, 303-328, 447-460:
+// element 0 = low 32 bits of block 0; block := (block & ~0xffffffff) |
+// bytes[16..20); element 1 = block mod m.
+struct EmitU32ModN64 {
+  static constexpr int kBN = 2;
+  __device__ static void Emit(const ExpandCtx& E, const uint32_t (&h)[2][4], uint32_t t,
+                              int64_t g) {
+    const VtDev& vt = E.vt;
+    if (g < E.a.leaf_begin || g >= E.a.leaf_end) return;
+    uint32_t v0 = h[0][0];
+    const uint64_t lo = (uint64_t)h[0][1] << 32 | h[1][0];
+    const uint64_t hi = (uint64_t)h[0][3] << 32 | h[0][2];
+    const uint64_t c = (uint64_t)vt.sc[1].fold_c;
+    const uint64_t mod = (uint64_t)vt.sc[1].mod;
+    // x = hi * 2^64 + lo = hi * c + lo (mod m); fold until it fits 64 bits.
+    uint64_t xlo = lo, xhi = hi;
+    while (xhi != 0) {
+      const uint64_t plo = xhi * c, phi = __umul64hi(xhi, c);
+      xlo = plo + xlo;
+      xhi = phi + (xlo < plo ? 1 : 0);
+    }
+    uint64_t v1 = xlo >= mod ? xlo - mod : xlo;
+    if (t) {
+      v0 += (uint32_t)vt.corr[0];
+      const uint64_t c1 = (uint64_t)vt.corr[1];
+      const uint64_t x = mod - c1;
+      v1 = v1 >= x ? v1 - x : v1 + c1;
+    }
+    if (vt.party == 1) {
+      v0 = 0u - v0;
+      v1 = v1 ? mod - v1 : 0;
+    }
+    char* dst = E.a.out + (g - E.a.leaf_begin) * (int64_t)vt.stride;
+    if (vt.sc[0].out_off == 8 && vt.sc[1].out_off == 0 && vt.stride == 16) {
+      *reinterpret_cast<uint4*>(dst) = make_uint4((uint32_t)v1, (uint32_t)(v1 >> 32), v0, 0u);
+    } else {
+      *reinterpret_cast<uint32_t*>(dst + vt.sc[0].out_off) = v0;
+      *reinterpret_cast<uint64_t*>(dst + vt.sc[1].out_off) = v1;
+    }
+  }
+};
+
+// ----------------------------------------------------------------------------
+// Fused subtree expansion kernel: each thread walks from its root to the root
+// of a 2^D-leaf subtree (both children computed, the path child kept), then
+// expands it depth-first in registers (right children kept per level), hashes
+// and emits every leaf.
+// ----------------------------------------------------------------------------
+
+template <int DEPTH, class Em>
+__device__ __forceinline__ void Dfs(const ExpandCtx& E, const uint32_t (&x)[4], uint32_t t,
+                                    int level, int64_t leaf) {
+  constexpr int BN = Em::kBN;
+  if constexpr (DEPTH == 0) {
+    uint32_t xs[1][4] = {{x[0], x[1], x[2], x[3]}};
+    uint32_t h[1][BN][4];
+    HashWords<1, BN>(xs, h, E.L);
+    Em::Emit(E, h[0], t, leaf);
+  } else {
+    const Cw cw = LoadCw(E.a.cw_seed, E.a.ccl, E.a.ccr, level);
+    uint32_t l[4], r[4], tl, tr;
+    Expand2(x, t, cw, E.L, l, tl, r, tr);
+    if constexpr (DEPTH == 1 && BN == 1) {
+      uint32_t xs[2][4] = {{l[0], l[1], l[2], l[3]}, {r[0], r[1], r[2], r[3]}};
+      uint32_t h[2][1][4];
+      HashWords<2, 1>(xs, h, E.L);
+      Em::Emit(E, h[0], tl, 2 * leaf);
+      Em::Emit(E, h[1], tr, 2 * leaf + 1);
+    } else {
+#pragma unroll 1
+      for (int b = 0; b < 2; ++b) {
+        uint32_t y[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) y[c] = b ? r[c] : l[c];
+        Dfs<DEPTH - 1, Em>(E, y, b ? tr : tl, level + 1, 2 * leaf + b);
+      }
+    }
+  }
+}
+
+template <int D, class Em>
+__global__ __launch_bounds__(kExpandBlock, kExpandWaves) void KExpand(ExpandArgs a, VtDev vt) {
+  __shared__ uint32_t tab[kTabWords];
+  FillTables(tab);
+  __syncthreads();
+  const Lds L = MakeLds(tab);
+  const ExpandCtx E{a, vt, L};
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t chunk = a.chunk_begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+       chunk < a.chunk_end; chunk += stride) {
+    const int64_t root = chunk >> a.walk;
+    const uint64_t path = (uint64_t)chunk & ((a.walk >= 63) ? ~0ull : ((1ull << a.walk) - 1));
+    uint4 s = a.root_seeds[root];
+    uint32_t x[4] = {s.x, s.y, s.z, s.w};
+    uint32_t t = a.root_cb[root];
+    for (int i = 0; i < a.walk; ++i) {
+      const uint32_t bit = (uint32_t)(path >> (a.walk - 1 - i)) & 1u;
+      const Cw cw = LoadCw(a.cw_seed, a.ccl, a.ccr, i);
+      uint32_t l[4], r[4], tl, tr;
+      Expand2(x, t, cw, L, l, tl, r, tr);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) x[c] = bit ? r[c] : l[c];
+      t = bit ? tr : tl;
+    }
+    Dfs<D, Em>(E, x, t, a.walk, chunk);
+  }
+}
+
+template <int D, class Em>
+int LaunchExpand(int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
+  hipLaunchKernelGGL((KExpand<D, Em>), dim3(grid), dim3(kExpandBlock), 0, st, a, vt);
+  return LaunchCheck("expand kernel launch");
+}
+
+template <class Em>
+int LaunchExpandAnyD(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
+  switch (D) {
+    case 0:
+      return LaunchExpand<0, Em>(grid, st, a, vt);
+    case 1:
+      return LaunchExpand<1, Em>(grid, st, a, vt);
+    case 2:
+      return LaunchExpand<2, Em>(grid, st, a, vt);
+    case 4:
+      return LaunchExpand<4, Em>(grid, st, a, vt);
+    default:
+      return LaunchExpand<8, Em>(grid, st, a, vt);
+  }
+}
+
+}  // namespace dpf_amd

@@ -1,0 +1,11 @@
+// k_expand_direct8.hip — KExpand for a directly convertible 8-byte integer or
+// XorWrapper value type (vth:216-228, 586-598).
+#include "expand_device.h"
+
+namespace dpf_amd {
+
+int LaunchExpandDirect8(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
+  return LaunchExpandAnyD<EmitDirect<8>>(D, grid, st, a, vt);
+}
+
+}  // namespace dpf_amd

@@ -1,0 +1,12 @@
+// k_expand_generic1.hip — KExpand with the descriptor-driven emitter for any
+// value type needing 1 hashed block(s) (tuples, IntModN, mixed widths).
+#include "expand_device.h"
+
+namespace dpf_amd {
+
+int LaunchExpandGeneric1(int D, int grid, hipStream_t st, const ExpandArgs& a,
+                         const VtDev& vt) {
+  return LaunchExpandAnyD<EmitGeneric<1>>(D, grid, st, a, vt);
+}
+
+}  // namespace dpf_amd

@@ -1,0 +1,122 @@
+// kernel_args.h — POD argument blocks of the gfx950 kernels and the host
+// launchers each kernel translation unit exports (the kernels are split over
+// several .hip files so hipcc compiles them in parallel).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "aes_tables.h"
+#include "internal.h"
+
+namespace dpf_amd {
+
+constexpr int kTabWords = 256 * 64;  // 64 KiB
+constexpr int kBlock = 256;  // 64 KiB LDS table per block; 2 blocks per CU
+#ifndef DPF_EXPAND_BLOCK
+#define DPF_EXPAND_BLOCK 256
+#define DPF_EXPAND_WAVES 2
+#endif
+// KExpand: threads per block and the minimum waves per SIMD the register
+// allocation must allow (2 blocks per CU share the CU's LDS).
+constexpr int kExpandBlock = DPF_EXPAND_BLOCK;
+constexpr int kExpandWaves = DPF_EXPAND_WAVES;
+
+struct KeyPair {
+  AesKey k[2];
+};
+
+struct ExpandArgs {
+  const uint4* root_seeds;
+  const uint8_t* root_cb;
+  const uint4* cw_seed;
+  const uint8_t* ccl;
+  const uint8_t* ccr;
+  char* out;
+  int64_t chunk_begin;
+  int64_t chunk_end;
+  int64_t leaf_begin;
+  int64_t leaf_end;
+  int32_t walk;  // levels walked per thread before the DFS
+  int32_t pad;
+};
+
+struct WalkArgs {
+  int64_t num_seeds;
+  int64_t num_cw;
+  const uint4* seeds_in;
+  const uint8_t* cb_in;
+  const uint4* paths;
+  const uint4* cw_seed;
+  const uint8_t* ccl;
+  const uint8_t* ccr;
+  uint4* seeds_out;
+  uint8_t* cb_out;
+  int32_t num_levels;
+  int32_t rightshift;
+};
+
+struct PointsArgs {
+  WalkArgs w;
+  const uint8_t* block_index;
+  const int8_t* party;
+  const uint4* value_corrections;  // per seed: epb * ns 128-bit words
+  char* out;
+};
+
+constexpr int kScanBlock = 256;
+constexpr int kScanWaves = kScanBlock / 64;
+constexpr int kScanUnroll = 8;
+constexpr int kFoldWords = 4;
+constexpr int kFoldSlices = 64;
+
+struct ScanArgs {
+  const uint4* db;
+  const uint4* sel;     // [query][selection_blocks]
+  uint4* partials;      // [blockIdx.x][query][C]
+  int64_t num_records;
+  int64_t sel_blocks;
+  int32_t C;            // 16-byte chunks per record
+  int32_t q0;           // first query of this pass
+  int32_t nq;           // queries in this pass (<= QN)
+  int32_t total_q;
+};
+
+inline int HipCheck(hipError_t e, const char* what) {
+  if (e == hipSuccess) return DPF_AMD_OK;
+  const int code =
+      (e == hipErrorOutOfMemory) ? DPF_AMD_RESOURCE_EXHAUSTED : DPF_AMD_INTERNAL;
+  return SetError(code, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+inline int LaunchCheck(const char* what) { return HipCheck(hipGetLastError(), what); }
+
+// k_expand_*.hip: fused expansion with DFS depth D in {0,1,2,4,8}.
+int LaunchExpandU32ModN64(int D, int grid, hipStream_t st, const ExpandArgs& a,
+                          const VtDev& vt);
+int LaunchExpandDirect1(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt);
+int LaunchExpandDirect2(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt);
+int LaunchExpandDirect4(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt);
+int LaunchExpandDirect8(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt);
+int LaunchExpandDirect16(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt);
+int LaunchExpandGeneric1(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt);
+int LaunchExpandGeneric2(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt);
+int LaunchExpandGeneric4(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt);
+// k_walk.hip
+int LaunchEvaluateSeeds(int grid, hipStream_t st, const WalkArgs& a, const KeyPair& kp);
+int LaunchEvaluatePoints(int bn, int grid, hipStream_t st, const PointsArgs& a,
+                         const VtDev& vt);
+int LaunchAesMmo(int grid, hipStream_t st, const uint4* in, uint4* out, int64_t n,
+                 const KeyPair& kp);
+// k_pir.hip
+int LaunchGatherRows(int grid, hipStream_t st, int64_t n, const int64_t* src_offset,
+                     int64_t opp, int64_t stride, const char* in, char* out);
+int LaunchXorFold(unsigned blocks, hipStream_t st, const uint4* parts, int num_parts,
+                  int64_t words, uint4* out);
+int LaunchXorFoldBytes(int grid, hipStream_t st, const uint8_t* parts, int num_parts,
+                       int64_t bytes, uint8_t* out);
+int LaunchPirScan(int nq, dim3 grid, hipStream_t st, const ScanArgs& a);
+
+}  // namespace dpf_amd

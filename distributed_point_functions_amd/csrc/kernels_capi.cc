@@ -1,0 +1,366 @@
+// kernels_capi.cc — the Tier-1 C ABI (include/dpf_amd.h): argument checks
+// with the reference's messages, device descriptors, grid sizing, and the
+// calls into the kernel launchers of k_*.hip.  No device code lives here.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <string>
+
+#include "aes_tables.h"
+#include "dpf_amd.h"
+#include "internal.h"
+#include "kernel_args.h"
+
+namespace dpf_amd {
+
+namespace {
+
+int GridFor(int64_t items, int block, int max_blocks) {
+  int64_t g = (items + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > max_blocks) g = max_blocks;
+  return (int)g;
+}
+
+KeyPair MakeKeyPair(uint64_t l_lo, uint64_t l_hi, uint64_t r_lo, uint64_t r_hi) {
+  KeyPair kp;
+  kp.k[0] = ExpandAesKey(l_lo, l_hi);
+  kp.k[1] = ExpandAesKey(r_lo, r_hi);
+  return kp;
+}
+
+int BnTemplate(int bn) {
+  if (bn <= 1) return 1;
+  if (bn == 2) return 2;
+  return 4;
+}
+
+// Picks the emitter for the value type.
+int LaunchExpandForType(int D, int grid, hipStream_t st, const ExpandArgs& a,
+                        const VtDev& vt) {
+  const bool single_direct = vt.direct && vt.ns == 1 && vt.sc[0].in_off == 0 &&
+                             vt.sc[0].out_off == 0 && vt.stride == vt.sc[0].bytes &&
+                             vt.bn == 1 && vt.epb * vt.sc[0].bytes == 16;
+  if (single_direct) {
+    switch (vt.sc[0].bytes) {
+      case 1:
+        return LaunchExpandDirect1(D, grid, st, a, vt);
+      case 2:
+        return LaunchExpandDirect2(D, grid, st, a, vt);
+      case 4:
+        return LaunchExpandDirect4(D, grid, st, a, vt);
+      case 8:
+        return LaunchExpandDirect8(D, grid, st, a, vt);
+      default:
+        return LaunchExpandDirect16(D, grid, st, a, vt);
+    }
+  }
+  const bool u32_modn64 =
+      !vt.direct && vt.ns == 2 && vt.bn == 2 && vt.epb == 1 &&
+      vt.sc[0].kind == DPF_AMD_KIND_INTEGER && vt.sc[0].bytes == 4 &&
+      vt.sc[1].kind == DPF_AMD_KIND_INT_MOD_N && vt.sc[1].bytes == 8 &&
+      vt.sc[1].use_fold && vt.sc[1].fold_w == 64 && (vt.sc[1].fold_c >> 56) == 0;
+  if (u32_modn64) return LaunchExpandU32ModN64(D, grid, st, a, vt);
+  switch (BnTemplate(vt.bn)) {
+    case 1:
+      return LaunchExpandGeneric1(D, grid, st, a, vt);
+    case 2:
+      return LaunchExpandGeneric2(D, grid, st, a, vt);
+    default:
+      return LaunchExpandGeneric4(D, grid, st, a, vt);
+  }
+}
+
+}  // namespace
+
+int MakeVtDev(const dpf_amd_value_type& vt, const uint64_t* correction, int party,
+              int cepb, VtDev* out) {
+  std::memset(out, 0, sizeof(*out));
+  if (vt.num_scalars <= 0 || vt.num_scalars > kMaxScalars)
+    return SetError(DPF_AMD_UNIMPLEMENTED, "unsupported number of tuple elements");
+  if (vt.elements_per_block * vt.num_scalars > kMaxCorrections)
+    return SetError(DPF_AMD_UNIMPLEMENTED, "too many packed elements");
+  if (vt.blocks_needed < 1 || vt.blocks_needed > DPF_AMD_MAX_BLOCKS_NEEDED)
+    return SetError(DPF_AMD_UNIMPLEMENTED, "blocks_needed out of supported range");
+  if (cepb < 1 || cepb > vt.elements_per_block)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "bad corrected_elements_per_block");
+  out->ns = vt.num_scalars;
+  out->direct = vt.directly_convertible;
+  out->epb = vt.elements_per_block;
+  out->esz = vt.element_size;
+  out->bn = vt.blocks_needed;
+  out->stride = vt.out_stride;
+  out->cepb = cepb;
+  out->party = party;
+  for (int s = 0; s < vt.num_scalars; ++s) {
+    const dpf_amd_scalar& in = vt.scalars[s];
+    ScalarDev& d = out->sc[s];
+    d.kind = in.kind;
+    d.bytes = in.bytes;
+    d.in_off = in.in_offset;
+    d.out_off = in.out_offset;
+    d.mod = (u128)in.modulus[0] | ((u128)in.modulus[1] << 64);
+    d.use_fold = 0;
+    if (in.kind == DPF_AMD_KIND_INT_MOD_N) {
+      if (d.mod == 0) return SetError(DPF_AMD_INVALID_ARGUMENT, "IntModN modulus is 0");
+      // w = bit length of (m - 1): m = 2^w - c with 0 <= c < 2^(w-1).
+      u128 mm = d.mod - 1;
+      int w = 0;
+      while (w < 128 && (mm >> w) != 0) ++w;
+      if (w >= 1 && w <= 127) {
+        u128 c = ((u128)1 << w) - d.mod;
+        if (w >= 8 && (c >> (w - 8)) == 0) {
+          d.use_fold = 1;
+          d.fold_w = w;
+          d.fold_c = c;
+        }
+      }
+    }
+  }
+  if (correction) {
+    for (int j = 0; j < vt.elements_per_block * vt.num_scalars; ++j)
+      out->corr[j] = (u128)correction[2 * j] | ((u128)correction[2 * j + 1] << 64);
+  }
+  out->corr_packed = 0;
+  if (vt.num_scalars == 1 && vt.scalars[0].bytes * vt.elements_per_block <= 16) {
+    const int b = vt.scalars[0].bytes;
+    for (int e = 0; e < vt.elements_per_block; ++e)
+      out->corr_packed |= (out->corr[e] & (b >= 16 ? ~(u128)0 : (((u128)1 << (8 * b)) - 1)))
+                          << (8 * b * e);
+  }
+  return DPF_AMD_OK;
+}
+
+}  // namespace dpf_amd
+
+using namespace dpf_amd;
+
+extern "C" {
+
+const char* dpf_amd_version(void) { return "dpf_amd 0.1 (gfx950, T-table AES in LDS)"; }
+
+int dpf_amd_device_count(int* count) {
+  return HipCheck(hipGetDeviceCount(count), "hipGetDeviceCount");
+}
+
+int dpf_amd_aes128_mmo(uint64_t key_lo, uint64_t key_hi, const void* in, void* out,
+                       int64_t n, void* stream) {
+  if (n < 0) return SetError(DPF_AMD_INVALID_ARGUMENT, "negative size");
+  if (n == 0) return DPF_AMD_OK;
+  if (!in || !out) return SetError(DPF_AMD_INVALID_ARGUMENT, "null buffer");
+  KeyPair kp = MakeKeyPair(key_lo, key_hi, key_lo, key_hi);
+  return LaunchAesMmo(GridFor(n, kBlock, 2048), (hipStream_t)stream, (const uint4*)in,
+                      (uint4*)out, n, kp);
+}
+
+int dpf_amd_evaluate_seeds(int64_t num_seeds, int num_levels, int64_t num_correction_words,
+                           const void* seeds_in, const uint8_t* control_bits_in,
+                           const void* paths, int paths_rightshift,
+                           const void* correction_seeds, const uint8_t* ccl,
+                           const uint8_t* ccr, uint64_t key_left_lo, uint64_t key_left_hi,
+                           uint64_t key_right_lo, uint64_t key_right_hi, void* seeds_out,
+                           uint8_t* control_bits_out, void* stream) {
+  if (num_correction_words != num_levels &&
+      num_correction_words != (int64_t)num_levels * num_seeds)
+    return SetError(DPF_AMD_INVALID_ARGUMENT,
+                    "`num_correction_words` must be equal to `num_levels` or "
+                    "`num_levels * num_seeds`");
+  if (num_seeds < 0 || num_levels < 0 || paths_rightshift < 0)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "negative size");
+  if (num_seeds == 0) return DPF_AMD_OK;
+  if (num_levels == 0) {
+    hipStream_t st = (hipStream_t)stream;
+    int rc = DPF_AMD_OK;
+    if (seeds_out != seeds_in)
+      rc = HipCheck(hipMemcpyAsync(seeds_out, seeds_in, 16 * num_seeds,
+                                   hipMemcpyDeviceToDevice, st), "copy");
+    if (rc == DPF_AMD_OK && control_bits_out != control_bits_in)
+      rc = HipCheck(hipMemcpyAsync(control_bits_out, control_bits_in, num_seeds,
+                                   hipMemcpyDeviceToDevice, st), "copy");
+    return rc;
+  }
+  WalkArgs a;
+  a.num_seeds = num_seeds;
+  a.num_cw = num_correction_words;
+  a.seeds_in = (const uint4*)seeds_in;
+  a.cb_in = control_bits_in;
+  a.paths = (const uint4*)paths;
+  a.cw_seed = (const uint4*)correction_seeds;
+  a.ccl = ccl;
+  a.ccr = ccr;
+  a.seeds_out = (uint4*)seeds_out;
+  a.cb_out = control_bits_out;
+  a.num_levels = num_levels;
+  a.rightshift = paths_rightshift;
+  KeyPair kp = MakeKeyPair(key_left_lo, key_left_hi, key_right_lo, key_right_hi);
+  return LaunchEvaluateSeeds(GridFor(num_seeds, kBlock, 4096), (hipStream_t)stream, a, kp);
+}
+
+int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
+                               const uint8_t* root_control_bits, int num_levels,
+                               const void* correction_seeds, const uint8_t* ccl,
+                               const uint8_t* ccr, const dpf_amd_value_type* vt,
+                               const uint64_t* value_correction, int party,
+                               int corrected_elements_per_block, int64_t leaf_begin,
+                               int64_t leaf_end, void* out, void* stream) {
+  if (num_levels < 0 || num_levels > 62)
+    return SetError(DPF_AMD_INVALID_ARGUMENT,
+                    "Trying to expand more than 62 tree levels at once. Please insert "
+                    "intermediate hierarchy levels, or evaluate fewer hierarchy levels "
+                    "at once.");
+  if (num_roots < 0 || !vt) return SetError(DPF_AMD_INVALID_ARGUMENT, "bad arguments");
+  if (num_roots > 0 && (num_roots > (INT64_MAX >> num_levels)))
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "Output size would be larger than 2**62.");
+  const int64_t total_leaves = num_roots << num_levels;
+  if (leaf_begin < 0 || leaf_end > total_leaves || leaf_begin > leaf_end)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "leaf range out of bounds");
+  if (leaf_begin == leaf_end) return DPF_AMD_OK;
+  VtDev dev;
+  int rc = MakeVtDev(*vt, value_correction, party, corrected_elements_per_block, &dev);
+  if (rc != DPF_AMD_OK) return rc;
+  // DFS depth D (compile-time); the upper num_levels - D levels are walked
+  // per thread (1 AES/level), amortised over 2^D leaves.
+  int D;
+  if (num_levels >= 8)
+    D = 8;
+  else if (num_levels >= 4)
+    D = 4;
+  else if (num_levels >= 2)
+    D = 2;
+  else
+    D = num_levels;
+  // For small problems prefer more threads over deep DFS.
+  while (D > 2 && ((leaf_end - leaf_begin) >> D) < 65536) D = (D == 8) ? 4 : 2;
+  ExpandArgs a;
+  a.root_seeds = (const uint4*)root_seeds;
+  a.root_cb = root_control_bits;
+  a.cw_seed = (const uint4*)correction_seeds;
+  a.ccl = ccl;
+  a.ccr = ccr;
+  a.out = (char*)out;
+  a.walk = num_levels - D;
+  a.pad = 0;
+  a.chunk_begin = leaf_begin >> D;
+  a.chunk_end = (leaf_end + (1ll << D) - 1) >> D;
+  a.leaf_begin = leaf_begin;
+  a.leaf_end = leaf_end;
+  const int grid = GridFor(a.chunk_end - a.chunk_begin, kExpandBlock, 8192 * 256 / kExpandBlock);
+  return LaunchExpandForType(D, grid, (hipStream_t)stream, a, dev);
+}
+
+int dpf_amd_evaluate_points(int64_t num_seeds, const void* seeds, const uint8_t* control_bits,
+                            const void* paths, int paths_rightshift, int num_levels,
+                            int64_t num_correction_words, const void* correction_seeds,
+                            const uint8_t* ccl, const uint8_t* ccr,
+                            const dpf_amd_value_type* vt, const uint8_t* block_index,
+                            const int8_t* party, int party_all,
+                            const void* value_corrections,
+                            const uint64_t* value_correction_all, void* out,
+                            void* seeds_out, uint8_t* control_bits_out, void* stream) {
+  if (num_correction_words != num_levels &&
+      num_correction_words != (int64_t)num_levels * num_seeds)
+    return SetError(DPF_AMD_INVALID_ARGUMENT,
+                    "`num_correction_words` must be equal to `num_levels` or "
+                    "`num_levels * num_seeds`");
+  if (num_seeds < 0 || num_levels < 0 || !vt)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "bad arguments");
+  if (num_seeds == 0) return DPF_AMD_OK;
+  VtDev dev;
+  int rc = MakeVtDev(*vt, value_correction_all, party_all, vt->elements_per_block, &dev);
+  if (rc != DPF_AMD_OK) return rc;
+  PointsArgs a;
+  a.w.num_seeds = num_seeds;
+  a.w.num_cw = num_correction_words;
+  a.w.seeds_in = (const uint4*)seeds;
+  a.w.cb_in = control_bits;
+  a.w.paths = (const uint4*)paths;
+  a.w.cw_seed = (const uint4*)correction_seeds;
+  a.w.ccl = ccl;
+  a.w.ccr = ccr;
+  a.w.seeds_out = (uint4*)seeds_out;
+  a.w.cb_out = control_bits_out;
+  a.w.num_levels = num_levels;
+  a.w.rightshift = paths_rightshift;
+  a.block_index = block_index;
+  a.party = party;
+  a.value_corrections = (const uint4*)value_corrections;
+  a.out = (char*)out;
+  const int grid = GridFor(num_seeds, kBlock, 4096);
+  hipStream_t st = (hipStream_t)stream;
+  return LaunchEvaluatePoints(BnTemplate(dev.bn), grid, st, a, dev);
+}
+
+int dpf_amd_gather_rows(int64_t num_prefixes, const int64_t* src_offset,
+                        int64_t outputs_per_prefix, int64_t stride, const void* in, void* out,
+                        void* stream) {
+  if (num_prefixes <= 0 || outputs_per_prefix <= 0) return DPF_AMD_OK;
+  const int64_t total = num_prefixes * outputs_per_prefix * stride;
+  return LaunchGatherRows(GridFor(total, 256, 8192), (hipStream_t)stream, num_prefixes,
+                          src_offset, outputs_per_prefix, stride, (const char*)in, (char*)out);
+}
+
+int dpf_amd_xor_fold(const void* parts, int num_parts, int64_t bytes, void* out,
+                     void* stream) {
+  if (num_parts <= 0 || bytes <= 0) return DPF_AMD_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (bytes % 16 == 0 && ((uintptr_t)parts % 16 == 0) && ((uintptr_t)out % 16 == 0)) {
+    const int64_t words = bytes / 16;
+    const int64_t blocks = (words + kFoldWords - 1) / kFoldWords;
+    if (blocks > INT32_MAX) return SetError(DPF_AMD_INVALID_ARGUMENT, "xor fold too large");
+    return LaunchXorFold((unsigned)blocks, st, (const uint4*)parts, num_parts, words,
+                         (uint4*)out);
+  }
+  return LaunchXorFoldBytes(GridFor(bytes, 256, 4096), st, (const uint8_t*)parts, num_parts,
+                            bytes, (uint8_t*)out);
+}
+
+static int ScanGrid(int64_t num_records) {
+  // ~8 resident 256-thread blocks per CU on 256 CUs; at least one tile per wave.
+  const int64_t tiles = (num_records + 127) / 128;
+  int64_t g = (tiles + kScanWaves - 1) / kScanWaves;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, 2048));
+}
+
+int64_t dpf_amd_inner_product_workspace_size(int64_t num_records, int64_t record_stride,
+                                             int num_queries) {
+  return (int64_t)ScanGrid(num_records) * num_queries * record_stride;
+}
+
+int dpf_amd_inner_product(const void* db, int64_t num_records, int64_t record_stride,
+                          const void* selections, int64_t selection_blocks, int num_queries,
+                          void* workspace, void* out, void* stream) {
+  if (num_queries == 0) return DPF_AMD_OK;
+  if (num_records < 0 || num_queries < 0)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "negative size");
+  if (record_stride <= 0 || record_stride % 16 != 0)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "record_stride must be a positive multiple of 16");
+  if (selection_blocks * 128 < num_records)
+    return SetError(DPF_AMD_INVALID_ARGUMENT,
+                    "`selections[0]` contains insufficient number of bits: " +
+                        std::to_string(selection_blocks * 128) +
+                        ", expected: " + std::to_string(num_records));
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = ScanGrid(num_records);
+  const int C = (int)(record_stride / 16);
+  ScanArgs a;
+  a.db = (const uint4*)db;
+  a.sel = (const uint4*)selections;
+  a.partials = (uint4*)workspace;
+  a.num_records = num_records;
+  a.sel_blocks = selection_blocks;
+  a.C = C;
+  a.total_q = num_queries;
+  const dim3 g(grid, (C + 63) / 64);
+  for (int q0 = 0; q0 < num_queries; q0 += 8) {
+    const int nq = std::min(8, num_queries - q0);
+    a.q0 = q0;
+    a.nq = nq;
+    int rc = LaunchPirScan(nq, g, st, a);
+    if (rc != DPF_AMD_OK) return rc;
+  }
+  return dpf_amd_xor_fold(workspace, grid, (int64_t)num_queries * record_stride, out, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,39 @@
+"""Builds A/B variants of one kernel translation unit into
+distributed_point_functions_amd/_native/var_<name>/libdpf_amd.so (select one
+at run time with DPF_AMD_LIB=<path>).  The other objects are the main build's.
+
+    python tools/build_variants.py k_expand_c5.hip name1:DEF=1,DEF2=3 name2:...
+"""
+import concurrent.futures
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from distributed_point_functions_amd import build_native as B  # noqa: E402
+
+
+def main():
+    tu = sys.argv[1]
+    B.build()
+    objs = [os.path.join(B.OBJ_DIR, os.path.basename(s) + ".o") for s in B._sources()]
+    others = [o for o in objs if os.path.basename(o) != tu + ".o"]
+
+    def one(spec):
+        name, _, defs = spec.partition(":")
+        d = os.path.join(B.OUT_DIR, "var_" + name)
+        os.makedirs(d, exist_ok=True)
+        obj = B._compile(os.path.join(B.CSRC, tu), True, d, [x for x in defs.split(",") if x])
+        lib = os.path.join(d, "libdpf_amd.so")
+        subprocess.check_call(["hipcc", "--offload-arch=" + B.ARCH, "-shared", "-fPIC", "-o", lib,
+                               obj] + others + ["-lpthread"])
+        return lib
+
+    with concurrent.futures.ThreadPoolExecutor(8) as ex:
+        for lib in ex.map(one, sys.argv[2:]):
+            print(lib)
+
+
+if __name__ == "__main__":
+    main()
