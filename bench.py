@@ -267,17 +267,25 @@ def main():
                        "leaves_per_step": leaves, "tree_levels": r["L"],
                        "parallelism": "independent keys, one 2^%d domain per GPU x%d" %
                                       (args.log_domain, world)},
-            "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS,
-                         "unit": "TOP/s", "frac": achieved / VALU_PEAK_TOPS,
+            # The T-table AES is bound by LDS lookup issue (ds_read_b32: 32
+            # lane-lookups/clk/CU, conflict-free by construction): achieved =
+            # algorithmic AES per launch x 160 lookups / kernel time.
+            "roofline": {"bound": "lds", "achieved": aes_s * LDS_LOOKUPS_PER_AES / 1e12,
+                         "peak": LDS_PEAK_LOOKUPS / 1e12, "unit": "T lookups/s",
+                         "frac": aes_s * LDS_LOOKUPS_PER_AES / LDS_PEAK_LOOKUPS,
                          "traffic": traffic_from_profiles("KExpand<8, dpf_amd::EmitU32ModN64>"),
                          "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/)",
                          "algorithmic_bytes": leaves // world * 16,
                          "kernel": "KExpand<8,EmitU32ModN64>", "kernel_ms": r["kernel_ms"],
+                         "aes_per_launch": aes_per_launch, "aes_per_leaf": AES_PER_LEAF_C5,
                          "aes_per_s_per_gpu": aes_s,
-                         "ops_per_aes": OPS_PER_AES,
-                         "lds_bound": {"achieved_lookups_per_s": aes_s * LDS_LOOKUPS_PER_AES,
-                                       "peak": LDS_PEAK_LOOKUPS,
-                                       "frac": aes_s * LDS_LOOKUPS_PER_AES / LDS_PEAK_LOOKUPS}},
+                         "lookups_per_aes": LDS_LOOKUPS_PER_AES,
+                         # implementation-independent view:
+                         # a bitsliced AES needs 757.5 gate ops per block
+                         "valu_equivalent": {"ops_per_aes": OPS_PER_AES,
+                                             "achieved_tops": achieved,
+                                             "peak_tops": VALU_PEAK_TOPS,
+                                             "frac": achieved / VALU_PEAK_TOPS}},
             "cpu_baseline": cpu,
         }
         if pir is not None:

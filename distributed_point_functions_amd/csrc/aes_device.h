@@ -21,6 +21,10 @@
 #include "internal.h"
 #include "kernel_args.h"
 
+#ifndef DPF_AES_SCHED
+#define DPF_AES_SCHED 1  // issue a round's table reads as one group
+#endif
+
 namespace dpf_amd {
 
 // One copy per translation unit (each .hip file is its own code object).
@@ -127,8 +131,10 @@ __device__ __forceinline__ void AesN(uint32_t (&w)[N][4], const K& key,
         t[n][c][2] = LoadT0(L, w[n][(c + 2) & 3], 2);
         t[n][c][3] = LoadT1(L, w[n][(c + 3) & 3], 3);
       }
+#if DPF_AES_SCHED
     __builtin_amdgcn_sched_group_barrier(0x002, 16 * N, 0);  // address VALU
     __builtin_amdgcn_sched_group_barrier(0x100, 16 * N, 0);  // DS reads
+#endif
 #pragma unroll
     for (int n = 0; n < N; ++n)
 #pragma unroll
@@ -147,8 +153,10 @@ __device__ __forceinline__ void AesN(uint32_t (&w)[N][4], const K& key,
       t[n][c][2] = LoadT0(L, w[n][(c + 2) & 3], 2);
       t[n][c][3] = LoadT1(L, w[n][(c + 3) & 3], 3);
     }
+#if DPF_AES_SCHED
   __builtin_amdgcn_sched_group_barrier(0x002, 16 * N, 0);
   __builtin_amdgcn_sched_group_barrier(0x100, 16 * N, 0);
+#endif
 #pragma unroll
   for (int n = 0; n < N; ++n)
 #pragma unroll

@@ -4,6 +4,11 @@
 // k_expand_*.hip translation units, each instantiating a few emitters.
 #pragma once
 
+// At 6 waves/SIMD the compiler's own interleaving of the table reads beats
+// forcing a round's reads into one group (fewer live VGPRs).
+#ifndef DPF_AES_SCHED
+#define DPF_AES_SCHED 0
+#endif
 #include "aes_device.h"
 
 namespace dpf_amd {
@@ -149,20 +154,22 @@ struct EmitU32ModN64 {
 
 // ----------------------------------------------------------------------------
 // Fused subtree expansion kernel: each thread walks from its root to the root
-// of a 2^D-leaf subtree (both children computed, the path child kept), then
-// expands it depth-first in registers (right children kept per level), hashes
-// and emits every leaf.
+// of a 2^D-leaf subtree (one AES per level, the path child only), then expands
+// it depth-first in registers (right children kept per level, their control
+// bit packed into the always-zero LSB of the seed), hashes and emits every
+// leaf.  The DFS position j is wave-uniform (an SGPR); a lane's leaf index is
+// (chunk << D) + j.
 // ----------------------------------------------------------------------------
 
-template <int DEPTH, class Em>
+template <int DEPTH, int D, class Em>
 __device__ __forceinline__ void Dfs(const ExpandCtx& E, const uint32_t (&x)[4], uint32_t t,
-                                    int level, int64_t leaf) {
+                                    int level, int64_t chunk, int j) {
   constexpr int BN = Em::kBN;
   if constexpr (DEPTH == 0) {
     uint32_t xs[1][4] = {{x[0], x[1], x[2], x[3]}};
     uint32_t h[1][BN][4];
     HashWords<1, BN>(xs, h, E.L);
-    Em::Emit(E, h[0], t, leaf);
+    Em::Emit(E, h[0], t, (chunk << D) + j);
   } else {
     const Cw cw = LoadCw(E.a.cw_seed, E.a.ccl, E.a.ccr, level);
     uint32_t l[4], r[4], tl, tr;
@@ -171,15 +178,22 @@ __device__ __forceinline__ void Dfs(const ExpandCtx& E, const uint32_t (&x)[4], 
       uint32_t xs[2][4] = {{l[0], l[1], l[2], l[3]}, {r[0], r[1], r[2], r[3]}};
       uint32_t h[2][1][4];
       HashWords<2, 1>(xs, h, E.L);
-      Em::Emit(E, h[0], tl, 2 * leaf);
-      Em::Emit(E, h[1], tr, 2 * leaf + 1);
+      Em::Emit(E, h[0], tl, (chunk << D) + 2 * j);
+      Em::Emit(E, h[1], tr, (chunk << D) + 2 * j + 1);
     } else {
+      // Only the right child stays live across the left recursion (its
+      // control bit packed into its seed's LSB); the left child is consumed
+      // by the first iteration.
+      r[0] |= tr;
+      uint32_t y[4] = {l[0], l[1], l[2], l[3]};
+      uint32_t ty = tl;
 #pragma unroll 1
       for (int b = 0; b < 2; ++b) {
-        uint32_t y[4];
+        Dfs<DEPTH - 1, D, Em>(E, y, ty, level + 1, chunk, 2 * j + b);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) y[c] = b ? r[c] : l[c];
-        Dfs<DEPTH - 1, Em>(E, y, b ? tr : tl, level + 1, 2 * leaf + b);
+        for (int c = 0; c < 4; ++c) y[c] = r[c];
+        ty = y[0] & 1u;
+        y[0] &= ~1u;
       }
     }
   }
@@ -193,23 +207,36 @@ __global__ __launch_bounds__(kExpandBlock, kExpandWaves) void KExpand(ExpandArgs
   const Lds L = MakeLds(tab);
   const ExpandCtx E{a, vt, L};
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t chunk = a.chunk_begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-       chunk < a.chunk_end; chunk += stride) {
-    const int64_t root = chunk >> a.walk;
-    const uint64_t path = (uint64_t)chunk & ((a.walk >= 63) ? ~0ull : ((1ull << a.walk) - 1));
+  // Every lane runs the same number of iterations (uniform trip count), so
+  // the per-level wave votes below see all lanes; lanes past the end idle.
+  const int64_t first = a.chunk_begin + (int64_t)blockIdx.x * blockDim.x;
+  for (int64_t base = first; base < a.chunk_end; base += stride) {
+    const int64_t chunk = base + threadIdx.x;
+    const bool live = chunk < a.chunk_end;
+    const int64_t c = live ? chunk : a.chunk_end - 1;
+    const int64_t root = c >> a.walk;
+    const uint64_t path = (uint64_t)c & ((a.walk >= 63) ? ~0ull : ((1ull << a.walk) - 1));
     uint4 s = a.root_seeds[root];
     uint32_t x[4] = {s.x, s.y, s.z, s.w};
     uint32_t t = a.root_cb[root];
     for (int i = 0; i < a.walk; ++i) {
       const uint32_t bit = (uint32_t)(path >> (a.walk - 1 - i)) & 1u;
       const Cw cw = LoadCw(a.cw_seed, a.ccl, a.ccr, i);
-      uint32_t l[4], r[4], tl, tr;
-      Expand2(x, t, cw, L, l, tl, r, tr);
+      // The upper path bits are shared by the whole wave: one AES with the
+      // key picked by a scalar select.  Lanes that disagree compute both
+      // children with the uniform keys and keep the path child.
+      if (__ballot(bit) == 0 || __ballot(bit ^ 1u) == 0) {
+        const uint32_t ubit = __builtin_amdgcn_readfirstlane(bit);
+        WalkStep(x, t, ubit, cw, DpfSelect{ubit != 0}, L);
+      } else {
+        uint32_t l[4], r[4], tl, tr;
+        Expand2(x, t, cw, L, l, tl, r, tr);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) x[c] = bit ? r[c] : l[c];
-      t = bit ? tr : tl;
+        for (int c = 0; c < 4; ++c) x[c] = bit ? r[c] : l[c];
+        t = bit ? tr : tl;
+      }
     }
-    Dfs<D, Em>(E, x, t, a.walk, chunk);
+    if (live) Dfs<D, D, Em>(E, x, t, a.walk, c, 0);
   }
 }
 

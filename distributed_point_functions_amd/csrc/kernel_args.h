@@ -16,11 +16,14 @@ namespace dpf_amd {
 constexpr int kTabWords = 256 * 64;  // 64 KiB
 constexpr int kBlock = 256;  // 64 KiB LDS table per block; 2 blocks per CU
 #ifndef DPF_EXPAND_BLOCK
-#define DPF_EXPAND_BLOCK 256
-#define DPF_EXPAND_WAVES 2
+#define DPF_EXPAND_BLOCK 768
+#define DPF_EXPAND_WAVES 6
 #endif
 // KExpand: threads per block and the minimum waves per SIMD the register
-// allocation must allow (2 blocks per CU share the CU's LDS).
+// allocation must allow.  Two blocks per CU (one 64 KiB table each) = 24
+// waves/CU = 6 per SIMD: the T-table reads need several waves per SIMD to
+// keep the LDS busy (measured: 2 waves/SIMD 19.4, 4: 23.6, 6: 24.0 G leaves/s
+// on c5; 8 waves spill more and gain nothing).
 constexpr int kExpandBlock = DPF_EXPAND_BLOCK;
 constexpr int kExpandWaves = DPF_EXPAND_WAVES;
 

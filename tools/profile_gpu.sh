@@ -20,5 +20,6 @@ run trace 400 --kernel-trace --stats
 run pmc_fetch 400 --pmc FETCH_SIZE
 run pmc_write 400 --pmc WRITE_SIZE
 run pmc_sq 400 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS
+run pmc_sq2 240 --pmc SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD
 run pmc_grbm 400 --pmc GRBM_GUI_ACTIVE GRBM_COUNT
 exit 0
