@@ -24,6 +24,12 @@
 #ifndef DPF_AES_SCHED
 #define DPF_AES_SCHED 1  // issue a round's table reads as one group
 #endif
+#ifndef DPF_VALUE_PAIRS
+#define DPF_VALUE_PAIRS 1  // AesPairs for the value PRG of even seeds
+#endif
+#ifndef DPF_LANE_WALK
+#define DPF_LANE_WALK 1  // divergent walk levels: 1 AES with a per-lane key
+#endif
 
 namespace dpf_amd {
 
@@ -112,35 +118,41 @@ struct PairSelect {  // generic keys from a kernel argument
 // (sched_group_barrier keeps the scheduler from splitting them into small
 // waitcnt-separated groups), then combines: per output column
 // T0[a] ^ T1[b] ^ rotl16(T0[c] ^ T1[d] ^ rotr16(rk)) = 2 v_bitop3 + 1 alignbit.
-template <int N, class K>
-__device__ __forceinline__ void AesN(uint32_t (&w)[N][4], const K& key,
-                                     const Lds& L) {
+// One full round r (1..9) of one state: the 16 lookups into t, then the
+// column combine into w.
+__device__ __forceinline__ void RoundLoads(const uint32_t (&w)[4], const Lds& L,
+                                           uint32_t (&t)[4][4]) {
 #pragma unroll
-  for (int n = 0; n < N; ++n)
+  for (int c = 0; c < 4; ++c) {
+    t[c][0] = LoadT0(L, w[c], 0);
+    t[c][1] = LoadT1(L, w[(c + 1) & 3], 1);
+    t[c][2] = LoadT0(L, w[(c + 2) & 3], 2);
+    t[c][3] = LoadT1(L, w[(c + 3) & 3], 3);
+  }
+}
+template <class K>
+__device__ __forceinline__ void RoundCombine(const uint32_t (&t)[4][4], const K& key, int n,
+                                             int r, uint32_t (&w)[4]) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) w[n][c] ^= key.rk(n, c);
+  for (int c = 0; c < 4; ++c)
+    w[c] = Xor3(t[c][0], t[c][1], Rotl16(Xor3(t[c][2], t[c][3], key.rkr(n, 4 * r + c))));
+}
+
+// Rounds R0..10 of N states (the states already hold round R0-1's output).
+template <int N, int R0, class K>
+__device__ __forceinline__ void AesFromRound(uint32_t (&w)[N][4], const K& key,
+                                             const Lds& L) {
 #pragma unroll
-  for (int r = 1; r < 10; ++r) {
+  for (int r = R0; r < 10; ++r) {
     uint32_t t[N][4][4];
 #pragma unroll
-    for (int n = 0; n < N; ++n)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        t[n][c][0] = LoadT0(L, w[n][c], 0);
-        t[n][c][1] = LoadT1(L, w[n][(c + 1) & 3], 1);
-        t[n][c][2] = LoadT0(L, w[n][(c + 2) & 3], 2);
-        t[n][c][3] = LoadT1(L, w[n][(c + 3) & 3], 3);
-      }
+    for (int n = 0; n < N; ++n) RoundLoads(w[n], L, t[n]);
 #if DPF_AES_SCHED
     __builtin_amdgcn_sched_group_barrier(0x002, 16 * N, 0);  // address VALU
     __builtin_amdgcn_sched_group_barrier(0x100, 16 * N, 0);  // DS reads
 #endif
 #pragma unroll
-    for (int n = 0; n < N; ++n)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        w[n][c] = Xor3(t[n][c][0], t[n][c][1],
-                       Rotl16(Xor3(t[n][c][2], t[n][c][3], key.rkr(n, 4 * r + c))));
+    for (int n = 0; n < N; ++n) RoundCombine(t[n], key, n, r, w[n]);
   }
   // Last round: S-box bytes are byte 1/2 of T0 and byte 3 of T1.
   uint32_t t[N][4][4];
@@ -165,6 +177,69 @@ __device__ __forceinline__ void AesN(uint32_t (&w)[N][4], const K& key,
       const uint32_t hi = __builtin_amdgcn_perm(t[n][c][3], t[n][c][2], 0x07020c0cu);
       w[n][c] = Xor3(lo, hi, key.rk(n, 40 + c));
     }
+}
+
+template <int N, class K>
+__device__ __forceinline__ void AesN(uint32_t (&w)[N][4], const K& key,
+                                     const Lds& L) {
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[n][c] ^= key.rk(n, c);
+  AesFromRound<N, 1>(w, key, L);
+}
+
+// NP pairs of blocks (w[2p], w[2p+1]) where w[2p+1] = w[2p] ^ (1 in bit 0 of
+// word 2): the value-PRG inputs sigma(s) and sigma(s + 1) of an even seed s
+// (cc:533-537; s + 1 only sets bit 0 of s.lo, i.e. bit 0 of sigma's byte 8).
+// After round 1 the odd state differs from the even one in column 2 only
+// (one lookup differs: T0 of byte 8); after round 2 each column differs by
+// one lookup.  So the odd block costs 1 + 4 lookups for rounds 1-2 instead
+// of 32: 133 instead of 160 lookups per odd block.  Keys: one fixed key.
+template <int NP, class K>
+__device__ __forceinline__ void AesPairs(uint32_t (&w)[2 * NP][4], const K& key,
+                                         const Lds& L) {
+  uint32_t e[NP][4], t[NP][4][4], x[NP][4];
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) e[p][c] = w[2 * p][c] ^ key.rk(0, c);
+  // Round 1: the even block's 16 lookups + T0 of the odd block's byte 8.
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    RoundLoads(e[p], L, t[p]);
+    x[p][0] = LoadT0(L, e[p][2] ^ 1u, 0);
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    RoundCombine(t[p], key, 0, 1, e[p]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[2 * p + 1][c] = e[p][c];
+    w[2 * p + 1][2] ^= t[p][2][0] ^ x[p][0];
+  }
+  // Round 2: the even block's 16 lookups + the 4 lookups of the odd
+  // block's column 2, which feeds T0 into column 2, T1 into column 1,
+  // T2 = rotl16(T0) into column 0 and T3 = rotl16(T1) into column 3.
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    RoundLoads(e[p], L, t[p]);
+    const uint32_t o = w[2 * p + 1][2];
+    x[p][0] = LoadT0(L, o, 0);
+    x[p][1] = LoadT1(L, o, 1);
+    x[p][2] = LoadT0(L, o, 2);
+    x[p][3] = LoadT1(L, o, 3);
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    RoundCombine(t[p], key, 0, 2, e[p]);
+    w[2 * p + 1][0] = e[p][0] ^ Rotl16(t[p][0][2] ^ x[p][2]);
+    w[2 * p + 1][1] = Xor3(e[p][1], t[p][1][1], x[p][1]);
+    w[2 * p + 1][2] = Xor3(e[p][2], t[p][2][0], x[p][0]);
+    w[2 * p + 1][3] = e[p][3] ^ Rotl16(t[p][3][3] ^ x[p][3]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[2 * p][c] = e[p][c];
+  }
+  AesFromRound<2 * NP, 3>(w, key, L);
 }
 
 // sigma(x) = (x.hi ^ x.lo, x.hi) (aes_128_fixed_key_hash.cc:75-78) in words.
@@ -437,7 +512,9 @@ struct ExpandCtx {
 };
 
 // Value PRG of one seed: block j = H_value(seed + j) (cc:523-547).
-template <int NS, int BN>
+// kEven: every seed has bit 0 clear (a seed whose control bit was just
+// extracted), so blocks (2i, 2i+1) go through AesPairs.
+template <int NS, int BN, bool kEven = false>
 __device__ __forceinline__ void HashWords(const uint32_t (&x)[NS][4],
                                           uint32_t (&h)[NS][BN][4], const Lds& L) {
   uint32_t st[NS * BN][4], sg[NS * BN][4];
@@ -457,7 +534,11 @@ __device__ __forceinline__ void HashWords(const uint32_t (&x)[NS][4],
       for (int c = 0; c < 4; ++c) st[n * BN + j][c] = sg[n * BN + j][c];
     }
   }
-  AesN<NS * BN>(st, DpfKeyAt<2>{}, L);
+  if constexpr (kEven && BN % 2 == 0 && DPF_VALUE_PAIRS) {
+    AesPairs<NS * BN / 2>(st, DpfKeyAt<2>{}, L);
+  } else {
+    AesN<NS * BN>(st, DpfKeyAt<2>{}, L);
+  }
 #pragma unroll
   for (int n = 0; n < NS; ++n)
 #pragma unroll

@@ -78,13 +78,28 @@ __device__ __forceinline__ void SwarNeg(uint32_t (&a)[4]) {
 // T is a single directly-convertible B-byte integer or XorWrapper
 // (uint8..uint128, XorWrapper<uint8..uint128>): the elements of a leaf are the
 // consecutive B-byte slices of the hashed block (vth:586-598).
+// One 16-byte leaf output in host layout (the packed emitters' common store).
+__device__ __forceinline__ void StoreLeaf16(const ExpandCtx& E, const uint4& v, int64_t g) {
+  if (g < E.a.leaf_begin || g >= E.a.leaf_end) return;
+  uint4* dst = reinterpret_cast<uint4*>(E.a.out) + (g - E.a.leaf_begin);
+#if DPF_EXPERIMENT_STORE == 1  // measurement only: almost no stores
+  if (v.z == 0x9e3779b9u) *dst = v;
+#elif DPF_EXPERIMENT_STORE == 2  // nontemporal stores
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 vv = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(dst));
+#else
+  *dst = v;
+#endif
+}
+
 template <int B>
 struct EmitDirect {
   static constexpr int kBN = 1;
-  __device__ static void Emit(const ExpandCtx& E, const uint32_t (&h)[1][4], uint32_t t,
-                              int64_t g) {
+  // Whole 16-byte blocks per leaf (every element of the block is returned).
+  __device__ static bool Packed(const VtDev& vt) { return vt.cepb * B == 16; }
+  __device__ static uint4 Value(const ExpandCtx& E, const uint32_t (&h)[1][4], uint32_t t) {
     const VtDev& vt = E.vt;
-    if (g < E.a.leaf_begin || g >= E.a.leaf_end) return;
     uint32_t w[4], c[4];
     const uint32_t m = 0u - t;
 #pragma unroll
@@ -99,13 +114,21 @@ struct EmitDirect {
       SwarAdd<B>(w, c);
       if (vt.party == 1) SwarNeg<B>(w);
     }
-    char* dst = E.a.out + (g - E.a.leaf_begin) * (int64_t)vt.cepb * B;
-    if (vt.cepb * B == 16) {
-      *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
-    } else {
-      const u128 v = ToU128(w);
-      for (int e = 0; e < vt.cepb; ++e) StoreScalar(dst + e * B, B, v >> (8 * B * e));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  __device__ static void Emit(const ExpandCtx& E, const uint32_t (&h)[1][4], uint32_t t,
+                              int64_t g) {
+    const VtDev& vt = E.vt;
+    const uint4 w = Value(E, h, t);
+    if (Packed(vt)) {
+      StoreLeaf16(E, w, g);
+      return;
     }
+    if (g < E.a.leaf_begin || g >= E.a.leaf_end) return;
+    char* dst = E.a.out + (g - E.a.leaf_begin) * (int64_t)vt.cepb * B;
+    const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+    const u128 v = ToU128(ww);
+    for (int e = 0; e < vt.cepb; ++e) StoreScalar(dst + e * B, B, v >> (8 * B * e));
   }
 };
 
@@ -115,11 +138,14 @@ struct EmitDirect {
 // bytes[16..20); element 1 = block mod m.
 struct EmitU32ModN64 {
   static constexpr int kBN = 2;
-  __device__ static void Emit(const ExpandCtx& E, const uint32_t (&h)[2][4], uint32_t t,
-                              int64_t g) {
+  // libstdc++ tuple layout: u64 at 0, u32 at 8, stride 16.
+  __device__ static bool Packed(const VtDev& vt) {
+    return vt.sc[0].out_off == 8 && vt.sc[1].out_off == 0 && vt.stride == 16;
+  }
+  __device__ static void Elements(const ExpandCtx& E, const uint32_t (&h)[2][4], uint32_t t,
+                                  uint32_t& v0, uint64_t& v1) {
     const VtDev& vt = E.vt;
-    if (g < E.a.leaf_begin || g >= E.a.leaf_end) return;
-    uint32_t v0 = h[0][0];
+    v0 = h[0][0];
     const uint64_t lo = (uint64_t)h[0][1] << 32 | h[1][0];
     const uint64_t hi = (uint64_t)h[0][3] << 32 | h[0][2];
     const uint64_t c = (uint64_t)vt.sc[1].fold_c;
@@ -131,7 +157,7 @@ struct EmitU32ModN64 {
       xlo = plo + xlo;
       xhi = phi + (xlo < plo ? 1 : 0);
     }
-    uint64_t v1 = xlo >= mod ? xlo - mod : xlo;
+    v1 = xlo >= mod ? xlo - mod : xlo;
     if (t) {
       v0 += (uint32_t)vt.corr[0];
       const uint64_t c1 = (uint64_t)vt.corr[1];
@@ -142,13 +168,27 @@ struct EmitU32ModN64 {
       v0 = 0u - v0;
       v1 = v1 ? mod - v1 : 0;
     }
-    char* dst = E.a.out + (g - E.a.leaf_begin) * (int64_t)vt.stride;
-    if (vt.sc[0].out_off == 8 && vt.sc[1].out_off == 0 && vt.stride == 16) {
-      *reinterpret_cast<uint4*>(dst) = make_uint4((uint32_t)v1, (uint32_t)(v1 >> 32), v0, 0u);
-    } else {
-      *reinterpret_cast<uint32_t*>(dst + vt.sc[0].out_off) = v0;
-      *reinterpret_cast<uint64_t*>(dst + vt.sc[1].out_off) = v1;
+  }
+  __device__ static uint4 Value(const ExpandCtx& E, const uint32_t (&h)[2][4], uint32_t t) {
+    uint32_t v0;
+    uint64_t v1;
+    Elements(E, h, t, v0, v1);
+    return make_uint4((uint32_t)v1, (uint32_t)(v1 >> 32), v0, 0u);
+  }
+  __device__ static void Emit(const ExpandCtx& E, const uint32_t (&h)[2][4], uint32_t t,
+                              int64_t g) {
+    const VtDev& vt = E.vt;
+    if (Packed(vt)) {
+      StoreLeaf16(E, Value(E, h, t), g);
+      return;
     }
+    if (g < E.a.leaf_begin || g >= E.a.leaf_end) return;
+    uint32_t v0;
+    uint64_t v1;
+    Elements(E, h, t, v0, v1);
+    char* dst = E.a.out + (g - E.a.leaf_begin) * (int64_t)vt.stride;
+    *reinterpret_cast<uint32_t*>(dst + vt.sc[0].out_off) = v0;
+    *reinterpret_cast<uint64_t*>(dst + vt.sc[1].out_off) = v1;
   }
 };
 
@@ -168,7 +208,8 @@ __device__ __forceinline__ void Dfs(const ExpandCtx& E, const uint32_t (&x)[4], 
   if constexpr (DEPTH == 0) {
     uint32_t xs[1][4] = {{x[0], x[1], x[2], x[3]}};
     uint32_t h[1][BN][4];
-    HashWords<1, BN>(xs, h, E.L);
+    // For D > 0 the seed comes out of Expand2 with its LSB cleared.
+    HashWords<1, BN, (D > 0)>(xs, h, E.L);
     Em::Emit(E, h[0], t, (chunk << D) + j);
   } else {
     const Cw cw = LoadCw(E.a.cw_seed, E.a.ccl, E.a.ccr, level);
@@ -228,6 +269,10 @@ __global__ __launch_bounds__(kExpandBlock, kExpandWaves) void KExpand(ExpandArgs
       if (__ballot(bit) == 0 || __ballot(bit ^ 1u) == 0) {
         const uint32_t ubit = __builtin_amdgcn_readfirstlane(bit);
         WalkStep(x, t, ubit, cw, DpfSelect{ubit != 0}, L);
+      } else if (DPF_LANE_WALK) {
+        // Divergent bits: one AES, round keys selected per lane (VALU
+        // v_cndmask per key word, no extra LDS lookups).
+        WalkStep(x, t, bit, cw, DpfSelect{bit != 0}, L);
       } else {
         uint32_t l[4], r[4], tl, tr;
         Expand2(x, t, cw, L, l, tl, r, tr);
