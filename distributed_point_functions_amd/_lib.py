@@ -92,6 +92,8 @@ def lib():
          ctypes.POINTER(ValueTypeDesc), P, I32, I32, I64, I64, P, P)
     _sig(L, "dpf_amd_evaluate_points", I32, I64, P, P, P, I32, I32, I64, P, P, P,
          ctypes.POINTER(ValueTypeDesc), P, P, I32, P, P, P, P, P, P)
+    _sig(L, "dpf_amd_evaluate_points_batched", I32, I64, I64, P, P, P, I32, I32, P, P, P,
+         ctypes.POINTER(ValueTypeDesc), P, P, I32, P, P, P, P)
     _sig(L, "dpf_amd_gather_rows", I32, I64, P, I64, I64, P, P, P)
     _sig(L, "dpf_amd_inner_product_workspace_size", I64, I64, I64, I32)
     _sig(L, "dpf_amd_inner_product", I32, P, I64, I64, P, I64, I32, P, P, P)

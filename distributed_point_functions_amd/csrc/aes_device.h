@@ -84,16 +84,21 @@ constexpr AesKey kDpfKeys[3] = {ExpandAesKey(kPrgKeyLeftLo, kPrgKeyLeftHi),
                                 ExpandAesKey(kPrgKeyValueLo, kPrgKeyValueHi)};
 
 // Key accessors: rk(n, i) / rkr(n, i) for state n, round-key word i.
+// post(n, i, w) is applied after round-key word i entered state n's word
+// (identity except for per-lane masked keys).
+struct KeyNoPost {
+  __device__ __forceinline__ uint32_t post(int, int, uint32_t w) const { return w; }
+};
 template <int W>
-struct DpfKeyAt {  // one fixed DPF key for all states
+struct DpfKeyAt : KeyNoPost {  // one fixed DPF key for all states
   __device__ __forceinline__ uint32_t rk(int, int i) const { return kDpfKeys[W].rk[i]; }
   __device__ __forceinline__ uint32_t rkr(int, int i) const { return kDpfKeys[W].rkr[i]; }
 };
-struct DpfLeftRight {  // state 0: left key, state 1: right key
+struct DpfLeftRight : KeyNoPost {  // state 0: left key, state 1: right key
   __device__ __forceinline__ uint32_t rk(int n, int i) const { return kDpfKeys[n].rk[i]; }
   __device__ __forceinline__ uint32_t rkr(int n, int i) const { return kDpfKeys[n].rkr[i]; }
 };
-struct DpfSelect {  // per-lane choice of the left / right key (path walk)
+struct DpfSelect : KeyNoPost {  // wave-uniform choice of the left / right key
   bool right;
   __device__ __forceinline__ uint32_t rk(int, int i) const {
     return right ? kDpfKeys[1].rk[i] : kDpfKeys[0].rk[i];
@@ -102,7 +107,7 @@ struct DpfSelect {  // per-lane choice of the left / right key (path walk)
     return right ? kDpfKeys[1].rkr[i] : kDpfKeys[0].rkr[i];
   }
 };
-struct PairSelect {  // generic keys from a kernel argument
+struct PairSelect : KeyNoPost {  // generic keys from a kernel argument
   const KeyPair& kp;
   bool right;
   __device__ __forceinline__ uint32_t rk(int, int i) const {
@@ -113,11 +118,29 @@ struct PairSelect {  // generic keys from a kernel argument
   }
 };
 
-// N independent AES-128 encryptions in lockstep.  Each round first forms all
-// 16N table addresses (v_perm), then issues all 16N ds_read_b32 back to back
-// (sched_group_barrier keeps the scheduler from splitting them into small
-// waitcnt-separated groups), then combines: per output column
-// T0[a] ^ T1[b] ^ rotl16(T0[c] ^ T1[d] ^ rotr16(rk)) = 2 v_bitop3 + 1 alignbit.
+// Per-lane choice of the left / right DPF key for N states: every round key
+// enters as the left key's word (an SGPR constant) and the lanes taking the
+// right key XOR in (left ^ right) under a lane mask — one VALU op per word,
+// no per-lane key words held in VGPRs.
+struct KeyDiff {
+  uint32_t d[44];
+};
+constexpr KeyDiff MakeKeyDiff() {
+  KeyDiff k{};
+  for (int i = 0; i < 44; ++i) k.d[i] = kDpfKeys[0].rk[i] ^ kDpfKeys[1].rk[i];
+  return k;
+}
+constexpr KeyDiff kDpfDiff = MakeKeyDiff();
+template <int N>
+struct DpfMasked {
+  uint32_t m[N];  // 0: left key, ~0: right key
+  __device__ __forceinline__ uint32_t rk(int, int i) const { return kDpfKeys[0].rk[i]; }
+  __device__ __forceinline__ uint32_t rkr(int, int i) const { return kDpfKeys[0].rkr[i]; }
+  __device__ __forceinline__ uint32_t post(int n, int i, uint32_t w) const {
+    return w ^ (kDpfDiff.d[i] & m[n]);
+  }
+};
+
 // One full round r (1..9) of one state: the 16 lookups into t, then the
 // column combine into w.
 __device__ __forceinline__ void RoundLoads(const uint32_t (&w)[4], const Lds& L,
@@ -135,10 +158,17 @@ __device__ __forceinline__ void RoundCombine(const uint32_t (&t)[4][4], const K&
                                              int r, uint32_t (&w)[4]) {
 #pragma unroll
   for (int c = 0; c < 4; ++c)
-    w[c] = Xor3(t[c][0], t[c][1], Rotl16(Xor3(t[c][2], t[c][3], key.rkr(n, 4 * r + c))));
+    w[c] = key.post(n, 4 * r + c,
+                    Xor3(t[c][0], t[c][1], Rotl16(Xor3(t[c][2], t[c][3], key.rkr(n, 4 * r + c)))));
 }
 
-// Rounds R0..10 of N states (the states already hold round R0-1's output).
+// N independent AES-128 encryptions in lockstep.  Each round first forms all
+// 16N table addresses (v_perm), then issues all 16N ds_read_b32 back to back
+// (sched_group_barrier keeps the scheduler from splitting them into small
+// waitcnt-separated groups), then combines: per output column
+// T0[a] ^ T1[b] ^ rotl16(T0[c] ^ T1[d] ^ rotr16(rk)) = 2 v_bitop3 + 1 alignbit.
+// AesFromRound runs rounds R0..10 (the states already hold round R0-1's
+// output).
 template <int N, int R0, class K>
 __device__ __forceinline__ void AesFromRound(uint32_t (&w)[N][4], const K& key,
                                              const Lds& L) {
@@ -175,7 +205,7 @@ __device__ __forceinline__ void AesFromRound(uint32_t (&w)[N][4], const K& key,
     for (int c = 0; c < 4; ++c) {
       const uint32_t lo = __builtin_amdgcn_perm(t[n][c][1], t[n][c][0], 0x0c0c0501u);
       const uint32_t hi = __builtin_amdgcn_perm(t[n][c][3], t[n][c][2], 0x07020c0cu);
-      w[n][c] = Xor3(lo, hi, key.rk(n, 40 + c));
+      w[n][c] = key.post(n, 40 + c, Xor3(lo, hi, key.rk(n, 40 + c)));
     }
 }
 
@@ -185,7 +215,7 @@ __device__ __forceinline__ void AesN(uint32_t (&w)[N][4], const K& key,
 #pragma unroll
   for (int n = 0; n < N; ++n)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) w[n][c] ^= key.rk(n, c);
+    for (int c = 0; c < 4; ++c) w[n][c] = key.post(n, c, w[n][c] ^ key.rk(n, c));
   AesFromRound<N, 1>(w, key, L);
 }
 

@@ -268,11 +268,11 @@ __global__ __launch_bounds__(kExpandBlock, kExpandWaves) void KExpand(ExpandArgs
       // children with the uniform keys and keep the path child.
       if (__ballot(bit) == 0 || __ballot(bit ^ 1u) == 0) {
         const uint32_t ubit = __builtin_amdgcn_readfirstlane(bit);
-        WalkStep(x, t, ubit, cw, DpfSelect{ubit != 0}, L);
+        WalkStep(x, t, ubit, cw, DpfSelect{{}, ubit != 0}, L);
       } else if (DPF_LANE_WALK) {
         // Divergent bits: one AES, round keys selected per lane (VALU
         // v_cndmask per key word, no extra LDS lookups).
-        WalkStep(x, t, bit, cw, DpfSelect{bit != 0}, L);
+        WalkStep(x, t, bit, cw, DpfMasked<1>{{0u - bit}}, L);
       } else {
         uint32_t l[4], r[4], tl, tr;
         Expand2(x, t, cw, L, l, tl, r, tr);

@@ -1,6 +1,14 @@
 // k_walk.hip — path-walk kernels: EvaluateSeeds (evaluate_prg_hwy.cc:552-634),
 // the fused EvaluateAt / EvaluateAndApply point evaluation and the plain
 // AES-MMO hash (aes_128_fixed_key_hash.cc:57-98).
+//
+// Both walks give each thread two points (i, i + T) walked in lockstep — two
+// independent AES chains per lane keep the LDS fed — when the launch has
+// more points than threads; a wave with no second point takes the one-state
+// path (the choice is wave-uniform).  The left/right PRG key is chosen per
+// lane from the path bit by masking the key difference into the state
+// (DpfMasked / PairMasked), one AES per level as the Highway walk
+// (evaluate_prg_hwy.cc:235-377).
 #include "aes_device.h"
 
 namespace dpf_amd {
@@ -11,76 +19,201 @@ __device__ __forceinline__ uint32_t PathBit(const uint4& p, int bit_index) {
   return (w >> (bit_index & 31)) & 1u;
 }
 
+// Per-lane choice between two generic keys of a kernel argument (the
+// differences are SALU work on SGPR words).
+template <int N>
+struct PairMasked {
+  const KeyPair& kp;
+  uint32_t m[N];
+  __device__ __forceinline__ uint32_t rk(int, int i) const { return kp.k[0].rk[i]; }
+  __device__ __forceinline__ uint32_t rkr(int, int i) const { return kp.k[0].rkr[i]; }
+  __device__ __forceinline__ uint32_t post(int n, int i, uint32_t w) const {
+    return w ^ ((kp.k[0].rk[i] ^ kp.k[1].rk[i]) & m[n]);
+  }
+};
+
+template <int N>
+struct DpfMaskedKeys {
+  __device__ __forceinline__ DpfMasked<N> operator()(const uint32_t (&m)[N]) const {
+    DpfMasked<N> k;
+#pragma unroll
+    for (int n = 0; n < N; ++n) k.m[n] = m[n];
+    return k;
+  }
+};
+template <int N>
+struct PairMaskedKeys {
+  const KeyPair& kp;
+  __device__ __forceinline__ PairMasked<N> operator()(const uint32_t (&m)[N]) const {
+    PairMasked<N> k{kp, {}};
+#pragma unroll
+    for (int n = 0; n < N; ++n) k.m[n] = m[n];
+    return k;
+  }
+};
+
+// NP points of one thread: their indices, the index of their per-seed (or
+// per-key) inputs, and the walk state.
+template <int NP>
+struct Walk {
+  int64_t idx[NP];
+  int64_t src[NP];
+  uint32_t x[NP][4];
+  uint32_t t[NP];
+};
+
+// Walks NP points num_levels levels (EvaluateSeeds semantics: level l uses
+// path bit num_levels - 1 - l + rightshift; correction words shared, per
+// seed [level][seed], or per key [key][level]).
+template <int NP, class KeyMaker>
+__device__ __forceinline__ void WalkPoints(const WalkArgs& w, Walk<NP>& s, const KeyMaker& km,
+                                           const Lds& L) {
+  const int64_t ppk = w.points_per_key;
+  const bool per_seed = ppk == 0 && w.num_cw > w.num_levels;
+  const int64_t cw_step = per_seed ? w.num_seeds : 1;
+  int64_t cw_base[NP];
+  uint4 p[NP];
+#pragma unroll
+  for (int n = 0; n < NP; ++n) {
+    s.src[n] = ppk > 0 ? s.idx[n] / ppk : s.idx[n];
+    cw_base[n] = ppk > 0 ? s.src[n] * w.num_levels : per_seed ? s.idx[n] : 0;
+    const uint4 v = w.seeds_in[s.src[n]];
+    s.x[n][0] = v.x;
+    s.x[n][1] = v.y;
+    s.x[n][2] = v.z;
+    s.x[n][3] = v.w;
+    s.t[n] = w.cb_in[s.src[n]];
+    p[n] = w.paths[s.idx[n]];
+  }
+  for (int level = 0; level < w.num_levels; ++level) {
+    const int bi = w.num_levels - level - 1 + w.rightshift;
+    uint32_t bit[NP], mask[NP];
+    Cw cw[NP];
+    uint32_t sg[NP][4], st[NP][4];
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+      bit[n] = PathBit(p[n], bi);
+      mask[n] = 0u - bit[n];
+      cw[n] = LoadCw(w.cw_seed, w.ccl, w.ccr, cw_base[n] + level * cw_step);
+      Sigma(s.x[n], sg[n]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) st[n][c] = sg[n][c];
+    }
+    AesN<NP>(st, km(mask), L);
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+      const uint32_t m = 0u - s.t[n];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s.x[n][c] = st[n][c] ^ sg[n][c] ^ (cw[n].seed[c] & m);
+      const uint32_t nt = (s.x[n][0] & 1u) ^ (s.t[n] & (bit[n] ? cw[n].cr : cw[n].cl));
+      s.x[n][0] &= ~1u;
+      s.t[n] = nt;
+    }
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ void StoreWalk(const WalkArgs& w, const Walk<NP>& s, int live) {
+#pragma unroll
+  for (int n = 0; n < NP; ++n) {
+    if (n >= live) break;
+    w.seeds_out[s.idx[n]] = make_uint4(s.x[n][0], s.x[n][1], s.x[n][2], s.x[n][3]);
+    w.cb_out[s.idx[n]] = (uint8_t)s.t[n];
+  }
+}
+
 // Generic-key EvaluateSeeds (evaluate_prg_hwy.cc:552-634).
-__global__ __launch_bounds__(kBlock, 2) void KEvaluateSeeds(WalkArgs a, KeyPair kp) {
+template <int NP>
+__device__ __forceinline__ void SeedsIter(const WalkArgs& w, const KeyPair& kp, const Lds& L,
+                                          int64_t base, int64_t T) {
+  Walk<NP> s;
+  const int live = (NP == 2 && base + T < w.num_seeds) ? 2 : 1;
+#pragma unroll
+  for (int n = 0; n < NP; ++n) s.idx[n] = n < live ? base + n * T : base;
+  WalkPoints<NP>(w, s, PairMaskedKeys<NP>{kp}, L);
+  StoreWalk<NP>(w, s, live);
+}
+
+__global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluateSeeds(WalkArgs a,
+                                                                              KeyPair kp) {
   __shared__ uint32_t tab[kTabWords];
   FillTables(tab);
   __syncthreads();
   const Lds L = MakeLds(tab);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.num_seeds;
-       i += stride) {
-    uint4 s = a.seeds_in[i];
-    uint32_t x[4] = {s.x, s.y, s.z, s.w};
-    uint32_t t = a.cb_in[i];
-    const uint4 p = a.paths[i];
-    const bool per_seed = a.num_cw > a.num_levels;
-    for (int level = 0; level < a.num_levels; ++level) {
-      const uint32_t bit = PathBit(p, a.num_levels - level - 1 + a.rightshift);
-      const int64_t ci = per_seed ? (int64_t)level * a.num_seeds + i : level;
-      const Cw cw = LoadCw(a.cw_seed, a.ccl, a.ccr, ci);
-      WalkStep(x, t, bit, cw, PairSelect{kp, bit != 0}, L);
+  const int64_t T = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; base < a.num_seeds;
+       base += 2 * T) {
+    if (__ballot(base + T < a.num_seeds) != 0) {
+      SeedsIter<2>(a, kp, L, base, T);
+    } else {
+      SeedsIter<1>(a, kp, L, base, T);
     }
-    a.seeds_out[i] = make_uint4(x[0], x[1], x[2], x[3]);
-    a.cb_out[i] = (uint8_t)t;
   }
 }
 
 // EvaluateAtImpl / EvaluateAndApply per-point evaluation (h:1013-1063,
-// 1143-1189).
+// 1143-1189): walk, value hash (HashExpandedSeeds), conversion + correction
+// of element block_index[i].
+template <int NP, int BN>
+__device__ __forceinline__ void PointsIter(const PointsArgs& a, const VtDev& vt, const Lds& L,
+                                           int64_t base, int64_t T) {
+  const WalkArgs& w = a.w;
+  Walk<NP> s;
+  const int live = (NP == 2 && base + T < w.num_seeds) ? 2 : 1;
+#pragma unroll
+  for (int n = 0; n < NP; ++n) s.idx[n] = n < live ? base + n * T : base;
+  WalkPoints<NP>(w, s, DpfMaskedKeys<NP>{}, L);
+  if (w.seeds_out) StoreWalk<NP>(w, s, live);
+  u128 W[NP][BN];
+  if constexpr (NP * BN <= 4) {
+    HashSeeds<NP, BN>(s.x, W, L);
+  } else {
+#pragma unroll
+    for (int n = 0; n < NP; ++n) {
+      const uint32_t xn[1][4] = {{s.x[n][0], s.x[n][1], s.x[n][2], s.x[n][3]}};
+      u128 Wn[1][BN];
+      HashSeeds<1, BN>(xn, Wn, L);
+#pragma unroll
+      for (int j = 0; j < BN; ++j) W[n][j] = Wn[0][j];
+    }
+  }
+  const int per_elem = vt.epb * vt.ns;
+#pragma unroll
+  for (int n = 0; n < NP; ++n) {
+    if (n >= live) break;
+    const int bi = a.block_index ? a.block_index[s.idx[n]] : 0;
+    const int party = a.party ? a.party[s.src[n]] : vt.party;
+    char* dst = a.out + s.idx[n] * (int64_t)vt.stride;
+    if (a.value_corrections) {
+      u128 corr[kMaxCorrections];
+      const uint4* c4 = a.value_corrections + s.src[n] * per_elem;
+      for (int j = 0; j < per_elem; ++j) {
+        const uint4 c = c4[j];
+        corr[j] = (u128)c.x | ((u128)c.y << 32) | ((u128)c.z << 64) | ((u128)c.w << 96);
+      }
+      EmitLeaf<BN>(vt, W[n], s.t[n] != 0, party, corr, bi, bi + 1,
+                   [dst](int) { return dst; });
+    } else {
+      EmitLeaf<BN>(vt, W[n], s.t[n] != 0, party, vt.corr, bi, bi + 1,
+                   [dst](int) { return dst; });
+    }
+  }
+}
+
 template <int BN>
-__global__ __launch_bounds__(kBlock, 2) void KEvaluatePoints(PointsArgs a, VtDev vt) {
+__global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluatePoints(PointsArgs a,
+                                                                               VtDev vt) {
   __shared__ uint32_t tab[kTabWords];
   FillTables(tab);
   __syncthreads();
   const Lds L = MakeLds(tab);
-  const WalkArgs& w = a.w;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int per_elem = vt.epb * vt.ns;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < w.num_seeds;
-       i += stride) {
-    uint4 s = w.seeds_in[i];
-    uint32_t x[1][4] = {{s.x, s.y, s.z, s.w}};
-    uint32_t t = w.cb_in[i];
-    const uint4 p = w.paths[i];
-    const bool per_seed = w.num_cw > w.num_levels;
-    for (int level = 0; level < w.num_levels; ++level) {
-      const uint32_t bit = PathBit(p, w.num_levels - level - 1 + w.rightshift);
-      const int64_t ci = per_seed ? (int64_t)level * w.num_seeds + i : level;
-      const Cw cw = LoadCw(w.cw_seed, w.ccl, w.ccr, ci);
-      WalkStep(x[0], t, bit, cw, DpfSelect{bit != 0}, L);
-    }
-    if (w.seeds_out) {
-      w.seeds_out[i] = make_uint4(x[0][0], x[0][1], x[0][2], x[0][3]);
-      w.cb_out[i] = (uint8_t)t;
-    }
-    u128 W[1][BN];
-    HashSeeds<1, BN>(x, W, L);
-    const int bi = a.block_index ? a.block_index[i] : 0;
-    const int party = a.party ? a.party[i] : vt.party;
-    char* dst = a.out + i * (int64_t)vt.stride;
-    if (a.value_corrections) {
-      u128 corr[kMaxCorrections];
-      const uint4* src = a.value_corrections + i * per_elem;
-      for (int j = 0; j < per_elem; ++j) {
-        uint4 c = src[j];
-        corr[j] = (u128)c.x | ((u128)c.y << 32) | ((u128)c.z << 64) | ((u128)c.w << 96);
-      }
-      EmitLeaf<BN>(vt, W[0], t != 0, party, corr, bi, bi + 1,
-                   [dst](int) { return dst; });
+  const int64_t T = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; base < a.w.num_seeds;
+       base += 2 * T) {
+    if (__ballot(base + T < a.w.num_seeds) != 0) {
+      PointsIter<2, BN>(a, vt, L, base, T);
     } else {
-      EmitLeaf<BN>(vt, W[0], t != 0, party, vt.corr, bi, bi + 1,
-                   [dst](int) { return dst; });
+      PointsIter<1, BN>(a, vt, L, base, T);
     }
   }
 }
@@ -99,27 +232,40 @@ __global__ __launch_bounds__(kBlock, 2) void KAesMmo(const uint4* in, uint4* out
     Sigma(x, s);
 #pragma unroll
     for (int c = 0; c < 4; ++c) st[0][c] = s[c];
-    AesN<1>(st, PairSelect{kp, false}, L);
+    AesN<1>(st, PairSelect{{}, kp, false}, L);
     out[i] = make_uint4(st[0][0] ^ s[0], st[0][1] ^ s[1], st[0][2] ^ s[2], st[0][3] ^ s[3]);
   }
 }
 
-int LaunchEvaluateSeeds(int grid, hipStream_t st, const WalkArgs& a, const KeyPair& kp) {
-  hipLaunchKernelGGL(KEvaluateSeeds, dim3(grid), dim3(kBlock), 0, st, a, kp);
+// Threads per block for a walk over n points: full blocks once the launch
+// fills every CU (two blocks each), smaller ones before that so that small
+// launches still spread over all CUs.
+static int WalkBlock(int64_t n) {
+  int64_t per = (n + 2 * 256 - 1) / (2 * 256);
+  per = (per + 63) / 64 * 64;
+  return (int)std::min<int64_t>(kPointsBlock, std::max<int64_t>(64, per));
+}
+
+int LaunchEvaluateSeeds(int64_t n, hipStream_t st, const WalkArgs& a, const KeyPair& kp) {
+  const int block = WalkBlock(n);
+  const int grid = (int)std::min<int64_t>(2 * 256, (n + block - 1) / block);
+  hipLaunchKernelGGL(KEvaluateSeeds, dim3(grid), dim3(block), 0, st, a, kp);
   return LaunchCheck("evaluate_seeds kernel launch");
 }
 
-int LaunchEvaluatePoints(int bn, int grid, hipStream_t st, const PointsArgs& a,
+int LaunchEvaluatePoints(int bn, int64_t n, hipStream_t st, const PointsArgs& a,
                          const VtDev& vt) {
+  const int block = WalkBlock(n);
+  const int grid = (int)std::min<int64_t>(2 * 256, (n + block - 1) / block);
   switch (bn) {
     case 1:
-      hipLaunchKernelGGL((KEvaluatePoints<1>), dim3(grid), dim3(kBlock), 0, st, a, vt);
+      hipLaunchKernelGGL((KEvaluatePoints<1>), dim3(grid), dim3(block), 0, st, a, vt);
       break;
     case 2:
-      hipLaunchKernelGGL((KEvaluatePoints<2>), dim3(grid), dim3(kBlock), 0, st, a, vt);
+      hipLaunchKernelGGL((KEvaluatePoints<2>), dim3(grid), dim3(block), 0, st, a, vt);
       break;
     default:
-      hipLaunchKernelGGL((KEvaluatePoints<4>), dim3(grid), dim3(kBlock), 0, st, a, vt);
+      hipLaunchKernelGGL((KEvaluatePoints<4>), dim3(grid), dim3(block), 0, st, a, vt);
   }
   return LaunchCheck("evaluate_points kernel launch");
 }

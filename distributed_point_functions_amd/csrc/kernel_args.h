@@ -57,6 +57,10 @@ struct WalkArgs {
   const uint8_t* ccr;
   uint4* seeds_out;
   uint8_t* cb_out;
+  // > 0: batched keys — point i belongs to key i / points_per_key; seeds_in,
+  // cb_in, party and value_corrections are per key and the correction words
+  // are [key][level].  0: per-seed / shared correction words (num_cw).
+  int64_t points_per_key;
   int32_t num_levels;
   int32_t rightshift;
 };
@@ -68,6 +72,11 @@ struct PointsArgs {
   const uint4* value_corrections;  // per seed: epb * ns 128-bit words
   char* out;
 };
+
+// KEvaluatePoints: 2 blocks per CU (one 64 KiB table each), 4 waves/SIMD,
+// two points per thread walked in lockstep.
+constexpr int kPointsBlock = 512;
+constexpr int kPointsWaves = 4;
 
 constexpr int kScanBlock = 256;
 constexpr int kScanWaves = kScanBlock / 64;
@@ -108,8 +117,8 @@ int LaunchExpandGeneric1(int D, int grid, hipStream_t st, const ExpandArgs& a, c
 int LaunchExpandGeneric2(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt);
 int LaunchExpandGeneric4(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt);
 // k_walk.hip
-int LaunchEvaluateSeeds(int grid, hipStream_t st, const WalkArgs& a, const KeyPair& kp);
-int LaunchEvaluatePoints(int bn, int grid, hipStream_t st, const PointsArgs& a,
+int LaunchEvaluateSeeds(int64_t n, hipStream_t st, const WalkArgs& a, const KeyPair& kp);
+int LaunchEvaluatePoints(int bn, int64_t n, hipStream_t st, const PointsArgs& a,
                          const VtDev& vt);
 int LaunchAesMmo(int grid, hipStream_t st, const uint4* in, uint4* out, int64_t n,
                  const KeyPair& kp);

@@ -192,10 +192,11 @@ int dpf_amd_evaluate_seeds(int64_t num_seeds, int num_levels, int64_t num_correc
   a.ccr = ccr;
   a.seeds_out = (uint4*)seeds_out;
   a.cb_out = control_bits_out;
+  a.points_per_key = 0;
   a.num_levels = num_levels;
   a.rightshift = paths_rightshift;
   KeyPair kp = MakeKeyPair(key_left_lo, key_left_hi, key_right_lo, key_right_hi);
-  return LaunchEvaluateSeeds(GridFor(num_seeds, kBlock, 4096), (hipStream_t)stream, a, kp);
+  return LaunchEvaluateSeeds(num_seeds, (hipStream_t)stream, a, kp);
 }
 
 int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
@@ -250,6 +251,42 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
   return LaunchExpandForType(D, grid, (hipStream_t)stream, a, dev);
 }
 
+// Shared body of dpf_amd_evaluate_points{,_batched}.
+static int EvaluatePoints(int64_t num_points, int64_t points_per_key, int64_t num_cw,
+                          const void* seeds, const uint8_t* control_bits, const void* paths,
+                          int paths_rightshift, int num_levels, const void* correction_seeds,
+                          const uint8_t* ccl, const uint8_t* ccr, const dpf_amd_value_type* vt,
+                          const uint8_t* block_index, const int8_t* party, int party_all,
+                          const void* value_corrections, const uint64_t* value_correction_all,
+                          void* out, void* seeds_out, uint8_t* control_bits_out,
+                          void* stream) {
+  if (num_points < 0 || num_levels < 0 || !vt)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "bad arguments");
+  if (num_points == 0) return DPF_AMD_OK;
+  VtDev dev;
+  int rc = MakeVtDev(*vt, value_correction_all, party_all, vt->elements_per_block, &dev);
+  if (rc != DPF_AMD_OK) return rc;
+  PointsArgs a;
+  a.w.num_seeds = num_points;
+  a.w.num_cw = num_cw;
+  a.w.seeds_in = (const uint4*)seeds;
+  a.w.cb_in = control_bits;
+  a.w.paths = (const uint4*)paths;
+  a.w.cw_seed = (const uint4*)correction_seeds;
+  a.w.ccl = ccl;
+  a.w.ccr = ccr;
+  a.w.seeds_out = (uint4*)seeds_out;
+  a.w.cb_out = control_bits_out;
+  a.w.points_per_key = points_per_key;
+  a.w.num_levels = num_levels;
+  a.w.rightshift = paths_rightshift;
+  a.block_index = block_index;
+  a.party = party;
+  a.value_corrections = (const uint4*)value_corrections;
+  a.out = (char*)out;
+  return LaunchEvaluatePoints(BnTemplate(dev.bn), num_points, (hipStream_t)stream, a, dev);
+}
+
 int dpf_amd_evaluate_points(int64_t num_seeds, const void* seeds, const uint8_t* control_bits,
                             const void* paths, int paths_rightshift, int num_levels,
                             int64_t num_correction_words, const void* correction_seeds,
@@ -264,32 +301,31 @@ int dpf_amd_evaluate_points(int64_t num_seeds, const void* seeds, const uint8_t*
     return SetError(DPF_AMD_INVALID_ARGUMENT,
                     "`num_correction_words` must be equal to `num_levels` or "
                     "`num_levels * num_seeds`");
-  if (num_seeds < 0 || num_levels < 0 || !vt)
-    return SetError(DPF_AMD_INVALID_ARGUMENT, "bad arguments");
-  if (num_seeds == 0) return DPF_AMD_OK;
-  VtDev dev;
-  int rc = MakeVtDev(*vt, value_correction_all, party_all, vt->elements_per_block, &dev);
-  if (rc != DPF_AMD_OK) return rc;
-  PointsArgs a;
-  a.w.num_seeds = num_seeds;
-  a.w.num_cw = num_correction_words;
-  a.w.seeds_in = (const uint4*)seeds;
-  a.w.cb_in = control_bits;
-  a.w.paths = (const uint4*)paths;
-  a.w.cw_seed = (const uint4*)correction_seeds;
-  a.w.ccl = ccl;
-  a.w.ccr = ccr;
-  a.w.seeds_out = (uint4*)seeds_out;
-  a.w.cb_out = control_bits_out;
-  a.w.num_levels = num_levels;
-  a.w.rightshift = paths_rightshift;
-  a.block_index = block_index;
-  a.party = party;
-  a.value_corrections = (const uint4*)value_corrections;
-  a.out = (char*)out;
-  const int grid = GridFor(num_seeds, kBlock, 4096);
-  hipStream_t st = (hipStream_t)stream;
-  return LaunchEvaluatePoints(BnTemplate(dev.bn), grid, st, a, dev);
+  return EvaluatePoints(num_seeds, 0, num_correction_words, seeds, control_bits, paths,
+                        paths_rightshift, num_levels, correction_seeds, ccl, ccr, vt,
+                        block_index, party, party_all, value_corrections, value_correction_all,
+                        out, seeds_out, control_bits_out, stream);
+}
+
+int dpf_amd_evaluate_points_batched(int64_t num_keys, int64_t points_per_key,
+                                    const void* key_seeds, const uint8_t* key_control_bits,
+                                    const void* paths, int paths_rightshift, int num_levels,
+                                    const void* correction_seeds, const uint8_t* ccl,
+                                    const uint8_t* ccr, const dpf_amd_value_type* vt,
+                                    const uint8_t* block_index, const int8_t* key_party,
+                                    int party_all, const void* key_value_corrections,
+                                    const uint64_t* value_correction_all, void* out,
+                                    void* stream) {
+  if (num_keys < 0 || points_per_key < 0)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "`num_keys` and `points_per_key` must be >= 0");
+  if (num_keys > 0 && points_per_key > INT64_MAX / num_keys)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "too many points");
+  if (num_keys == 0 || points_per_key == 0) return DPF_AMD_OK;
+  return EvaluatePoints(num_keys * points_per_key, points_per_key, num_keys * num_levels,
+                        key_seeds, key_control_bits, paths, paths_rightshift, num_levels,
+                        correction_seeds, ccl, ccr, vt, block_index, key_party, party_all,
+                        key_value_corrections, value_correction_all, out, nullptr, nullptr,
+                        stream);
 }
 
 int dpf_amd_gather_rows(int64_t num_prefixes, const int64_t* src_offset,

@@ -116,6 +116,25 @@ def evaluate_points(seeds, control_bits, paths, paths_rightshift, num_levels,
     return out
 
 
+def evaluate_points_batched(num_keys: int, points_per_key: int, key_seeds, key_control_bits,
+                            paths, paths_rightshift: int, num_levels: int, cw_seeds, ccl, ccr,
+                            desc, block_index=None, key_party=None, party_all: int = 0,
+                            key_value_corrections=None, value_correction_all=(), out=None):
+    """Batched EvaluateAt over num_keys keys (dpf_amd_evaluate_points_batched):
+    point k * points_per_key + j belongs to key k; correction words are
+    [key][level] arrays."""
+    n = num_keys * points_per_key
+    if out is None:
+        out = torch.empty(n * desc.out_stride, dtype=torch.uint8, device=paths.device)
+    corr = _corr_words(value_correction_all)
+    check(_lib.lib().dpf_amd_evaluate_points_batched(
+        num_keys, points_per_key, dptr(key_seeds), dptr(key_control_bits), dptr(paths),
+        paths_rightshift, num_levels, dptr(cw_seeds), dptr(ccl), dptr(ccr), ctypes.byref(desc),
+        dptr(block_index), dptr(key_party), party_all, dptr(key_value_corrections),
+        corr.ctypes.data_as(ctypes.c_void_p), dptr(out), stream_ptr()))
+    return out
+
+
 def inner_product(db: torch.Tensor, num_records: int, record_stride: int,
                   selections: torch.Tensor, num_queries: int,
                   workspace: torch.Tensor = None, out: torch.Tensor = None):

@@ -148,6 +148,24 @@ int dpf_amd_evaluate_points(
     const void* value_corrections, const uint64_t* value_correction_all,
     void* out, void* seeds_out, uint8_t* control_bits_out, void* stream);
 
+/* Batched EvaluateAt over `num_keys` keys of one DPF (the per-key loop a
+ * caller of EvaluateAtImpl h:913-1070 runs, as one launch): point
+ * i = k * points_per_key + j belongs to key k.  Per-key device arrays:
+ * key_seeds, key_control_bits, key_party (NULL = `party_all`),
+ * key_value_corrections (epb * num_scalars words per key; NULL =
+ * `value_correction_all`), and the correction words laid out [key][level]
+ * (num_keys * num_levels each).  Per-point: paths, block_index (NULL = 0),
+ * out (one host-layout T per point). */
+int dpf_amd_evaluate_points_batched(
+    int64_t num_keys, int64_t points_per_key, const void* key_seeds,
+    const uint8_t* key_control_bits, const void* paths, int paths_rightshift,
+    int num_levels, const void* correction_seeds,
+    const uint8_t* correction_controls_left,
+    const uint8_t* correction_controls_right, const dpf_amd_value_type* vt,
+    const uint8_t* block_index, const int8_t* key_party, int party_all,
+    const void* key_value_corrections, const uint64_t* value_correction_all,
+    void* out, void* stream);
+
 /* Gathers the per-prefix output slices of an incremental evaluation
  * (h:877-889): out[i * opp + k] = in[src_offset[i] + k] for k < opp, rows of
  * `stride` bytes. */

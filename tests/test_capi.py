@@ -21,7 +21,7 @@ def test_header_declares_the_boundary():
     names = declared_functions()
     assert len(names) >= 40
     for must in ("dpf_amd_evaluate_seeds", "dpf_amd_expand_and_correct",
-                 "dpf_amd_evaluate_points", "dpf_amd_inner_product",
+                 "dpf_amd_evaluate_points", "dpf_amd_evaluate_points_batched", "dpf_amd_inner_product",
                  "dpf_amd_evaluate_until", "dpf_amd_pir_server_handle_request"):
         assert must in names
 

@@ -234,6 +234,56 @@ def test_evaluate_points_matches_oracle(K, cuda, spec, ld):
         assert got == want
 
 
+@pytest.mark.parametrize("spec", [TYPES[0], TYPES[3], TYPES[4], TYPES[13], TYPES[17]],
+                         ids=[repr(t) for t in (TYPES[0], TYPES[3], TYPES[4], TYPES[13],
+                                                TYPES[17])])
+@pytest.mark.parametrize("ld,nkeys,ppk", [(1, 3, 5), (32, 7, 37), (128, 4, 129),
+                                          (20, 5, 70001)])
+def test_evaluate_points_batched_matches_oracle(K, cuda, spec, ld, nkeys, ppk):
+    """One launch over several keys (alternating parties) == the oracle's
+    per-key EvaluateAt.  The last case has > 2^18 points, so threads walk two
+    points each (the i / i + T pairing)."""
+    from distributed_point_functions_amd import value_types as vtm
+    vt = vtm.from_spec(spec)
+    rng = random.Random(ld * 31 + nkeys)
+    keys = []
+    for k in range(nkeys):
+        d, k0, k1, alpha, beta = _keys(spec, ld, seed=k + 2)
+        keys.append((d, (k0, k1)[k % 2], alpha))
+    d = keys[0][0]
+    L = d.hierarchy_to_tree(0)
+    epb = d.elements_per_block(0)
+    bbits = ld - L
+    maxp = (1 << ld) - 1
+    pts = []
+    for k in range(nkeys):
+        p = [rng.getrandbits(128) & maxp for _ in range(ppk)]
+        p[0] = keys[k][2]
+        pts.append(p)
+    flat = [p for ps in pts for p in ps]
+    tree = [p >> bbits if epb > 1 else p for p in flat]
+    bi = [p & ((1 << bbits) - 1) if epb > 1 else 0 for p in flat]
+    ks = [k for _, k, _ in keys]
+    cws = [c for k in ks for c in (k.cw_seeds()[:L] or [0])]
+    ccl = [c for k in ks for c in (k.ccl()[:L] or [0])]
+    ccr = [c for k in ks for c in (k.ccr()[:L] or [0])]
+    import torch
+    out = K.evaluate_points_batched(
+        nkeys, ppk, K.u128_tensor([k.seed for k in ks], cuda), u8([k.party for k in ks], cuda),
+        K.u128_tensor(tree, cuda), 0, L, K.u128_tensor(cws, cuda), u8(ccl, cuda), u8(ccr, cuda),
+        vt.descriptor(d.blocks_needed(0)), block_index=u8(bi, cuda),
+        key_party=torch.tensor([k.party for k in ks], dtype=torch.int8, device=cuda),
+        key_value_corrections=K.u128_tensor(
+            [c for k in ks for c in k.value_corrections()[0]], cuda))
+    got = vt.decode_flat(out.cpu().numpy().view(vt.numpy_dtype()))
+    step = max(1, ppk // 300)
+    for k in range(nkeys):
+        sample = list(range(0, ppk, step)) + [ppk - 1]
+        # keys of one spec/ld share parameters, so any key's Dpf evaluates
+        want = keys[k][0].evaluate_at(ks[k], 0, [pts[k][j] for j in sample])
+        assert [got[k * ppk + j] for j in sample] == want, k
+
+
 # ---------------------------------------------------------------------------
 # Dense PIR scan vs oracle InnerProduct
 # ---------------------------------------------------------------------------

@@ -1,0 +1,275 @@
+"""Measures the secondary BASELINE.json configs on one MI355X (the headline c5
+and c4 Q=1 lines are bench.py's).  One JSON line per config on stdout.
+
+    python tools/bench_configs.py [--only c1,c2,c3,c4q]
+
+c1  full-domain EvaluateNext, log_domain 20, uint64 (1.5 AES/leaf)
+c2  EvaluateAt of 2^20 random points over 64 keys, log_domain 128, uint128
+    (129 AES/point); Tier-1 (device arrays, one launch per key and one
+    multi-key launch) and Tier-2 (the EvaluateAt API, host vectors)
+c3  incremental heavy hitters: 16 levels 8,16,..,128 bits, uint64, 2^16
+    surviving prefixes per level (generator of distributed_point_function_
+    benchmark.cc:154-191, distinct prefixes); Tier-2 EvaluateNext per level
+c4q dense-PIR XOR scan at Q = 8 and 64 over 2^26 x 256 B (kernel only)
+
+Kernel times are HIP events on the launch stream; API times are wall clock.
+Every config also checks its outputs (share-sum / reconstruction).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from distributed_point_functions_amd import _lib, kernels  # noqa: E402
+from distributed_point_functions_amd import value_types as V  # noqa: E402
+from distributed_point_functions_amd.dpf import (  # noqa: E402
+    DistributedPointFunction, DpfParameters, decode_value)
+
+LDS_PEAK_LOOKUPS = 256 * 32 * 2.4e9
+M64 = (1 << 64) - 1
+
+
+def ev_time(fn, reps):
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    e0.record(st)
+    for _ in range(reps):
+        fn()
+    e1.record(st)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps / 1e3
+
+
+def wall_time(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps
+
+
+def key_dev(dpf, key, level, dev):
+    L = dpf.hierarchy_to_tree(level)
+    cws = key.correction_words[:L]
+    vt = dpf.parameters[level].value_type
+    corr = [x for v in key.last_level_value_correction for x in decode_value(vt, v)]
+    return dict(
+        L=L,
+        seed=kernels.u128_tensor([key.seed], dev),
+        cb=torch.tensor([key.party], dtype=torch.uint8, device=dev),
+        cw=kernels.u128_tensor([c.seed for c in cws] or [0], dev),
+        ccl=torch.tensor([int(c.control_left) for c in cws] or [0], dtype=torch.uint8, device=dev),
+        ccr=torch.tensor([int(c.control_right) for c in cws] or [0], dtype=torch.uint8, device=dev),
+        corr=corr, party=key.party)
+
+
+def lds_frac(aes_per_s):
+    return aes_per_s * 160 / LDS_PEAK_LOOKUPS
+
+
+def c1(dev, reps):
+    dpf = DistributedPointFunction.create(DpfParameters(20, V.Integer(64)))
+    k0, k1 = dpf.generate_keys(777777, 123456789123, seeds=(0x51, 0x52))
+    desc = dpf.value_type_descriptor(0)
+    ka = key_dev(dpf, k0, 0, dev)
+    L = ka["L"]
+    cepb = 1 << (20 - L)
+    out = torch.empty((1 << 20) * 8, dtype=torch.uint8, device=dev)
+
+    def step():
+        kernels.expand_and_correct(ka["seed"], ka["cb"], L, ka["cw"], ka["ccl"], ka["ccr"],
+                                   desc, ka["corr"], ka["party"], cepb, 0, 1 << L, out)
+    t_k = ev_time(step, reps)
+    ctx_reps = max(1, reps // 4)
+
+    def api():
+        dpf.evaluate_next([], dpf.create_evaluation_context(k0), raw=True)
+    t_api = wall_time(api, ctx_reps)
+    a = dpf.evaluate_next([], dpf.create_evaluation_context(k0), raw=True).view(np.uint64)
+    b = dpf.evaluate_next([], dpf.create_evaluation_context(k1), raw=True).view(np.uint64)
+    s = a + b
+    ok = bool(s[777777] == 123456789123 and np.count_nonzero(s) == 1)
+    aes = 2 * ((1 << L) - 1) + (1 << L)
+    return {"config": "c1", "workload": "full-domain EvaluateNext log_domain=20 uint64",
+            "leaves": 1 << 20, "kernel_ms": t_k * 1e3, "leaves_per_s": (1 << 20) / t_k,
+            "api_ms": t_api * 1e3, "api_leaves_per_s": (1 << 20) / t_api,
+            "aes_per_leaf": aes / (1 << 20), "lds_frac": lds_frac(aes / t_k), "correct": ok}
+
+
+def c2(dev, reps):
+    rng = random.Random(2)
+    nkeys, per = 64, 1 << 14
+    vt = V.Integer(128)
+    dpf = DistributedPointFunction.create(DpfParameters(128, vt))
+    desc = dpf.value_type_descriptor(0)
+    keys, kd, pts = [], [], []
+    for k in range(nkeys):
+        alpha, beta = rng.getrandbits(128), rng.getrandbits(128)
+        k0, k1 = dpf.generate_keys(alpha, beta, seeds=(1000 + 2 * k, 1001 + 2 * k))
+        p = [rng.getrandbits(128) for _ in range(per)]
+        p[0] = alpha
+        keys.append((k0, k1, alpha, beta))
+        kd.append(key_dev(dpf, k0, 0, dev))
+        pts.append(kernels.u128_tensor(p, dev))
+    L = kd[0]["L"]
+    seeds = [kernels.u128_tensor([keys[k][0].seed] * per, dev) for k in range(nkeys)]
+    cbs = [torch.full((per,), keys[k][0].party, dtype=torch.uint8, device=dev)
+           for k in range(nkeys)]
+    out = torch.empty(nkeys * per * 16, dtype=torch.uint8, device=dev)
+
+    def tier1():
+        for k in range(nkeys):
+            kernels.evaluate_points(seeds[k], cbs[k], pts[k], 0, L, kd[k]["cw"], kd[k]["ccl"],
+                                    kd[k]["ccr"], desc, party_all=kd[k]["party"],
+                                    value_correction_all=kd[k]["corr"],
+                                    out=out[k * per * 16:(k + 1) * per * 16])
+    t1 = ev_time(tier1, reps)
+    res = {"config": "c2", "workload": "EvaluateAt 2^20 points / 64 keys, log_domain=128, uint128",
+           "points": nkeys * per, "aes_per_point": L + 1,
+           "tier1_per_key_ms": t1 * 1e3, "tier1_per_key_points_per_s": nkeys * per / t1,
+           "tier1_per_key_lds_frac": lds_frac(nkeys * per * (L + 1) / t1)}
+    if hasattr(kernels, "evaluate_points_batched"):
+        allp = torch.cat(pts)
+        cw = torch.cat([d["cw"] for d in kd])
+        ccl = torch.cat([d["ccl"] for d in kd])
+        ccr = torch.cat([d["ccr"] for d in kd])
+        kseed = torch.cat([d["seed"] for d in kd])
+        kcb = torch.cat([d["cb"] for d in kd])
+        kcorr = kernels.u128_tensor([x for d in kd for x in d["corr"]], dev)
+
+        def multi():
+            kernels.evaluate_points_batched(nkeys, per, kseed, kcb, allp, 0, L, cw, ccl, ccr,
+                                            desc, party_all=0, key_value_corrections=kcorr,
+                                            out=out)
+        tm = ev_time(multi, reps)
+        res.update({"tier1_multi_key_ms": tm * 1e3,
+                    "tier1_multi_key_points_per_s": nkeys * per / tm,
+                    "tier1_multi_key_lds_frac": lds_frac(nkeys * per * (L + 1) / tm)})
+        got = out.view(torch.int64).view(-1, 2).cpu().numpy().view(np.uint64)
+    plist = [kernels.tensor_u128(p) for p in pts]
+
+    def tier2():
+        for k in range(nkeys):
+            dpf.evaluate_at(keys[k][0], 0, plist[k], raw=True)
+    t2 = wall_time(tier2, max(1, reps // 4))
+    ok = True
+    for k in range(0, nkeys, 16):
+        a = dpf.evaluate_at(keys[k][0], 0, plist[k][:64], raw=True)
+        b = dpf.evaluate_at(keys[k][1], 0, plist[k][:64], raw=True)
+        s = [(vt.decode(a)[i] + vt.decode(b)[i]) % (1 << 128) for i in range(64)]
+        ok &= s[0] == keys[k][3] and all(x == 0 for x in s[1:])
+        if "tier1_multi_key_ms" in res:
+            w = got[k * per:k * per + 64]
+            ok &= [int(lo) | (int(hi) << 64) for lo, hi in w] == vt.decode(a)
+    res.update({"tier2_api_ms": t2 * 1e3, "tier2_api_points_per_s": nkeys * per / t2,
+                "correct": bool(ok)})
+    return res
+
+
+def c3(dev, reps):
+    rng = random.Random(3)
+    H = 16
+    params = [DpfParameters(8 * (i + 1), V.Integer(64)) for i in range(H)]
+    dpf = DistributedPointFunction.create_incremental(params)
+    alpha = rng.getrandbits(128)
+    betas = [rng.getrandbits(64) for _ in range(H)]
+    k0, k1 = dpf.generate_keys_incremental(alpha, betas, seeds=(0x31, 0x32))
+    prefixes = [[]]
+    for i in range(1, H):
+        if i == 1:
+            cur = list(range(256))
+        else:
+            cur = set()
+            prev = prefixes[i - 1]
+            while len(cur) < (1 << 16):
+                cur.add((prev[rng.randrange(len(prev))] << 8) | rng.randrange(256))
+            cur = sorted(cur)
+        # keep alpha's prefix so the check below sees the non-zero
+        ap = alpha >> (128 - 8 * i)
+        if ap not in cur:
+            cur[rng.randrange(len(cur))] = ap
+            cur = sorted(cur)
+        prefixes.append(cur)
+
+    def run(key, keep=False):
+        ctx = dpf.create_evaluation_context(key)
+        outs, times = [], []
+        for i in range(H):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            o = dpf.evaluate_next(prefixes[i], ctx, raw=True)
+            times.append(time.perf_counter() - t0)
+            if keep:
+                outs.append(o.view(np.uint64).copy())
+        return outs, times
+    run(k0)
+    best = None
+    for _ in range(max(1, reps // 4)):
+        _, times = run(k0)
+        best = times if best is None or sum(times) < sum(best) else best
+    a, _ = run(k0, True)
+    b, _ = run(k1, True)
+    ok = True
+    for i in range(H):
+        s = a[i] + b[i]
+        nz = np.nonzero(s)[0]
+        ok &= len(nz) == 1 and int(s[nz[0]]) == betas[i]
+    leaves = sum(len(x) for x in a)
+    return {"config": "c3", "workload": "heavy hitters, 16 levels x 8 bits, uint64, 2^16 prefixes",
+            "returned_leaves": leaves, "api_ms_total": 1e3 * sum(best),
+            "api_ms_per_level": [round(1e3 * t, 3) for t in best],
+            "api_leaves_per_s": leaves / sum(best), "correct": bool(ok)}
+
+
+def c4q(dev, reps):
+    n, rec = 1 << 26, 256
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(4)
+    db = torch.randint(0, 256, (n * rec,), dtype=torch.uint8, device=dev, generator=gen)
+    res = {"config": "c4q", "workload": "XOR scan 2^26 x 256 B"}
+    for q in (1, 8, 64):
+        sel = torch.randint(-2**63, 2**63 - 1, (q * (n // 128), 2), dtype=torch.int64,
+                            device=dev, generator=gen)
+        ws = torch.empty(max(16, _lib.lib().dpf_amd_inner_product_workspace_size(n, rec, q)),
+                         dtype=torch.uint8, device=dev)
+        out = torch.empty(q * rec, dtype=torch.uint8, device=dev)
+
+        def scan():
+            kernels.inner_product(db, n, rec, sel, q, ws, out)
+        t = ev_time(scan, reps)
+        res["q%d_ms" % q] = t * 1e3
+        res["q%d_db_GBps" % q] = n * rec / t / 1e9
+        res["q%d_hbm_frac" % q] = (n * rec + q * n // 8) / t / 8e12
+        res["q%d_query_GBps" % q] = q * n * rec / t / 1e9
+    del db
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="c1,c2,c3,c4q")
+    ap.add_argument("--reps", type=int, default=8)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    for name in args.only.split(","):
+        r = globals()[name](dev, args.reps)
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
