@@ -127,6 +127,8 @@ def _bind_tier2(L):
     _sig(L, "dpf_amd_ctx_num_partial_evaluations", I64, P)
     _sig(L, "dpf_amd_evaluate_until", I32, P, I32, P, I64, P, SZ, P, P, I64,
          ctypes.POINTER(I64))
+    _sig(L, "dpf_amd_evaluate_until_device", I32, P, I32, P, I64, P, SZ, P, P, I64,
+         ctypes.POINTER(I64), P)
     _sig(L, "dpf_amd_evaluate_at", I32, P, P, SZ, I32, P, I64, P, SZ, P)
     _sig(L, "dpf_amd_evaluate_and_apply", I32, P, P, P, I64, P, I32, P, SZ, P)
     _sig(L, "dpf_amd_pir_db_create", I32, PP)

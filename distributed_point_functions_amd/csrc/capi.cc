@@ -166,10 +166,11 @@ int64_t dpf_amd_ctx_num_partial_evaluations(const dpf_amd_ctx* ctx) {
   return ctx->ctx.partial_evaluations_size();
 }
 
-int dpf_amd_evaluate_until(const dpf_amd_dpf* dpf, int hierarchy_level,
+static int EvaluateUntilImpl(const dpf_amd_dpf* dpf, int hierarchy_level,
                            const uint64_t* prefixes, int64_t num_prefixes,
                            const uint8_t* value_type, size_t value_type_len, dpf_amd_ctx* ctx,
-                           void* out, int64_t out_capacity, int64_t* num_outputs) {
+                           void* out, int64_t out_capacity, int64_t* num_outputs,
+                           bool out_on_device, void* stream) {
   ValueType t;
   int rc = ParseType(value_type, value_type_len, &t);
   if (rc != DPF_AMD_OK) return rc;
@@ -182,8 +183,26 @@ int dpf_amd_evaluate_until(const dpf_amd_dpf* dpf, int hierarchy_level,
   const dpf_amd_value_type layout = dpf->dpf->value_type_descriptor(lvl);
   const int64_t cap = layout.out_stride > 0 ? out_capacity / layout.out_stride : 0;
   st = dpf->dpf->EvaluateUntilRaw(hierarchy_level, Span<const uint128>(p.data(), p.size()),
-                                  ctx->ctx, layout, out, cap, num_outputs, false, nullptr);
+                                  ctx->ctx, layout, out, cap, num_outputs, out_on_device, stream);
   return st.ok() ? DPF_AMD_OK : Fail(st);
+}
+
+int dpf_amd_evaluate_until(const dpf_amd_dpf* dpf, int hierarchy_level,
+                           const uint64_t* prefixes, int64_t num_prefixes,
+                           const uint8_t* value_type, size_t value_type_len, dpf_amd_ctx* ctx,
+                           void* out, int64_t out_capacity, int64_t* num_outputs) {
+  return EvaluateUntilImpl(dpf, hierarchy_level, prefixes, num_prefixes, value_type,
+                           value_type_len, ctx, out, out_capacity, num_outputs, false, nullptr);
+}
+
+int dpf_amd_evaluate_until_device(const dpf_amd_dpf* dpf, int hierarchy_level,
+                                  const uint64_t* prefixes, int64_t num_prefixes,
+                                  const uint8_t* value_type, size_t value_type_len,
+                                  dpf_amd_ctx* ctx, void* out_device, int64_t out_capacity,
+                                  int64_t* num_outputs, void* stream) {
+  return EvaluateUntilImpl(dpf, hierarchy_level, prefixes, num_prefixes, value_type,
+                           value_type_len, ctx, out_device, out_capacity, num_outputs, true,
+                           stream);
 }
 
 int dpf_amd_evaluate_at(const dpf_amd_dpf* dpf, const uint8_t* key, size_t key_len,

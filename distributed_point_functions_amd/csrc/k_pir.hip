@@ -88,6 +88,36 @@ __device__ __forceinline__ uint32_t SelWord(const uint4& s, int idx) {
   return idx == 0 ? s.x : idx == 1 ? s.y : idx == 2 ? s.z : s.w;
 }
 
+// Folds the per-lane accumulators of a block into partials
+// [block][query][chunk]: lanes that share a chunk, then the block's waves,
+// through LDS.
+template <int QN>
+__device__ __forceinline__ void FoldPartials(const ScanArgs& a, const uint4 (&acc)[QN],
+                                             uint4* red, int Cs, int G, bool active,
+                                             int chunk_lo) {
+  for (int q = 0; q < a.nq && q < QN; ++q) {
+    uint4 mine = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int qq = 0; qq < QN; ++qq)
+      if (qq == q) mine = acc[qq];
+    red[threadIdx.x] = active ? mine : make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    if (threadIdx.x < Cs) {
+      uint4 r = make_uint4(0, 0, 0, 0);
+      for (int w = 0; w < kScanWaves; ++w)
+        for (int g = 0; g < G; ++g) {
+          uint4 x = red[w * 64 + g * Cs + threadIdx.x];
+          r.x ^= x.x;
+          r.y ^= x.y;
+          r.z ^= x.z;
+          r.w ^= x.w;
+        }
+      a.partials[((int64_t)blockIdx.x * a.total_q + a.q0 + q) * a.C + chunk_lo + threadIdx.x] = r;
+    }
+    __syncthreads();
+  }
+}
+
 template <int QN>
 __global__ __launch_bounds__(kScanBlock) void KPirScan(ScanArgs a) {
   __shared__ uint4 red[kScanBlock];
@@ -136,28 +166,68 @@ __global__ __launch_bounds__(kScanBlock) void KPirScan(ScanArgs a) {
       }
     }
   }
-  // Fold lanes that share a chunk, then waves, through LDS.
-  for (int q = 0; q < a.nq && q < QN; ++q) {
-    uint4 mine = make_uint4(0, 0, 0, 0);
+  FoldPartials<QN>(a, acc, red, Cs, G, active, chunk_lo);
+}
+
+// Fast path for record widths of C = 64 / G chunks (G = 2..32 records per
+// wave-instruction) or C a multiple of 64 (G = 1, slices of 64 chunks).  The
+// records of one wave-instruction never straddle a 32-record selection word,
+// so each query's word is wave-uniform (SGPRs) and a lane's mask is one
+// signed bit-field extract; up to 16 queries per pass.
+template <int QN, int G>
+__global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
+  constexpr int Cs = 64 / G;
+  constexpr int U = (G * 8 <= 32) ? 8 : 32 / G;  // loads in flight per lane
+  __shared__ uint4 red[kScanBlock];
+  const int lane = threadIdx.x & 63;
+  // wave-uniform by construction; readfirstlane lets the compiler see it, so
+  // the selection words below are scalar loads into SGPRs
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int chunk_lo = blockIdx.y * 64;
+  const int my_chunk = chunk_lo + (lane % Cs);
+  const int my_rec = lane / Cs;
+  const uint32_t* sel = reinterpret_cast<const uint32_t*>(a.sel);
+  uint4 acc[QN];
 #pragma unroll
-    for (int qq = 0; qq < QN; ++qq)
-      if (qq == q) mine = acc[qq];
-    red[threadIdx.x] = active ? mine : make_uint4(0, 0, 0, 0);
-    __syncthreads();
-    if (threadIdx.x < Cs) {
-      uint4 r = make_uint4(0, 0, 0, 0);
-      for (int w = 0; w < kScanWaves; ++w)
-        for (int g = 0; g < G; ++g) {
-          uint4 x = red[w * 64 + g * Cs + threadIdx.x];
-          r.x ^= x.x;
-          r.y ^= x.y;
-          r.z ^= x.z;
-          r.w ^= x.w;
+  for (int q = 0; q < QN; ++q) acc[q] = make_uint4(0, 0, 0, 0);
+  const int64_t tiles = (a.num_records + 127) >> 7;
+  const int64_t wstride = (int64_t)gridDim.x * kScanWaves;
+  for (int64_t tile = (int64_t)blockIdx.x * kScanWaves + wave; tile < tiles; tile += wstride) {
+    const int64_t rec0 = tile << 7;
+    const bool full = rec0 + 128 <= a.num_records;
+#pragma unroll 1
+    for (int d = 0; d < 4; ++d) {
+      // selection word d (records rec0 + 32d ..) of each query
+      uint32_t word[QN];
+#pragma unroll
+      for (int q = 0; q < QN; ++q)
+        word[q] = (q < a.nq) ? sel[((int64_t)(a.q0 + q) * a.sel_blocks + tile) * 4 + d] : 0u;
+#pragma unroll 1
+      for (int k0 = 0; k0 < 32; k0 += G * U) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t rec = rec0 + d * 32 + k0 + u * G + my_rec;
+          v[u] = (full || rec < a.num_records) ? a.db[rec * a.C + my_chunk]
+                                                : make_uint4(0, 0, 0, 0);
         }
-      a.partials[((int64_t)blockIdx.x * a.total_q + a.q0 + q) * a.C + chunk_lo + threadIdx.x] = r;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int bit = k0 + u * G + my_rec;
+#pragma unroll
+          for (int q = 0; q < QN; ++q) {
+            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)word[q], bit, 1);
+            // acc ^= v & m as one v_bitop3 (truth table src0 ^ (src1 & src2))
+            acc[q].x = __builtin_amdgcn_bitop3_b32(acc[q].x, v[u].x, m, 0x78);
+            acc[q].y = __builtin_amdgcn_bitop3_b32(acc[q].y, v[u].y, m, 0x78);
+            acc[q].z = __builtin_amdgcn_bitop3_b32(acc[q].z, v[u].z, m, 0x78);
+            acc[q].w = __builtin_amdgcn_bitop3_b32(acc[q].w, v[u].w, m, 0x78);
+          }
+        }
+      }
     }
-    __syncthreads();
   }
+  FoldPartials<QN>(a, acc, red, Cs, G, true, chunk_lo);
 }
 
 int LaunchGatherRows(int grid, hipStream_t st, int64_t n, const int64_t* src_offset,
@@ -180,15 +250,64 @@ int LaunchXorFoldBytes(int grid, hipStream_t st, const uint8_t* parts, int num_p
   return LaunchCheck("xor fold kernel launch");
 }
 
-int LaunchPirScan(int nq, dim3 g, hipStream_t st, const ScanArgs& a) {
+template <int G>
+static void LaunchScanG(int nq, dim3 g, hipStream_t st, const ScanArgs& a) {
   if (nq == 1)
-    hipLaunchKernelGGL((KPirScan<1>), g, dim3(kScanBlock), 0, st, a);
+    hipLaunchKernelGGL((KPirScanG<1, G>), g, dim3(kScanBlock), 0, st, a);
   else if (nq <= 2)
-    hipLaunchKernelGGL((KPirScan<2>), g, dim3(kScanBlock), 0, st, a);
+    hipLaunchKernelGGL((KPirScanG<2, G>), g, dim3(kScanBlock), 0, st, a);
   else if (nq <= 4)
-    hipLaunchKernelGGL((KPirScan<4>), g, dim3(kScanBlock), 0, st, a);
+    hipLaunchKernelGGL((KPirScanG<4, G>), g, dim3(kScanBlock), 0, st, a);
+  else if (nq <= 8)
+    hipLaunchKernelGGL((KPirScanG<8, G>), g, dim3(kScanBlock), 0, st, a);
   else
-    hipLaunchKernelGGL((KPirScan<8>), g, dim3(kScanBlock), 0, st, a);
+    hipLaunchKernelGGL((KPirScanG<16, G>), g, dim3(kScanBlock), 0, st, a);
+}
+
+int PirScanGroup(int C) {
+  if (C % 64 == 0) return 1;
+  switch (C) {
+    case 2:
+    case 4:
+    case 8:
+    case 16:
+    case 32:
+      return 64 / C;
+    default:
+      return 0;
+  }
+}
+
+int LaunchPirScan(int nq, dim3 g, hipStream_t st, const ScanArgs& a) {
+  switch (PirScanGroup(a.C)) {
+    case 1:
+      LaunchScanG<1>(nq, g, st, a);
+      break;
+    case 2:
+      LaunchScanG<2>(nq, g, st, a);
+      break;
+    case 4:
+      LaunchScanG<4>(nq, g, st, a);
+      break;
+    case 8:
+      LaunchScanG<8>(nq, g, st, a);
+      break;
+    case 16:
+      LaunchScanG<16>(nq, g, st, a);
+      break;
+    case 32:
+      LaunchScanG<32>(nq, g, st, a);
+      break;
+    default:
+      if (nq == 1)
+        hipLaunchKernelGGL((KPirScan<1>), g, dim3(kScanBlock), 0, st, a);
+      else if (nq <= 2)
+        hipLaunchKernelGGL((KPirScan<2>), g, dim3(kScanBlock), 0, st, a);
+      else if (nq <= 4)
+        hipLaunchKernelGGL((KPirScan<4>), g, dim3(kScanBlock), 0, st, a);
+      else
+        hipLaunchKernelGGL((KPirScan<8>), g, dim3(kScanBlock), 0, st, a);
+  }
   return LaunchCheck("pir scan kernel launch");
 }
 

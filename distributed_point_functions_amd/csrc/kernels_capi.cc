@@ -389,8 +389,9 @@ int dpf_amd_inner_product(const void* db, int64_t num_records, int64_t record_st
   a.C = C;
   a.total_q = num_queries;
   const dim3 g(grid, (C + 63) / 64);
-  for (int q0 = 0; q0 < num_queries; q0 += 8) {
-    const int nq = std::min(8, num_queries - q0);
+  const int per_pass = PirScanQueries(C);
+  for (int q0 = 0; q0 < num_queries; q0 += per_pass) {
+    const int nq = std::min(per_pass, num_queries - q0);
     a.q0 = q0;
     a.nq = nq;
     int rc = LaunchPirScan(nq, g, st, a);

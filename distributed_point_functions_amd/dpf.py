@@ -89,6 +89,11 @@ class DpfKey:
         return DpfKey(out)
 
 
+def _seq(values):
+    """128-bit inputs: an (n, 2) uint64 {lo, hi} array as is, else a list."""
+    return values if isinstance(values, np.ndarray) else list(values)
+
+
 def decode_value(vt: ValueType, data: bytes):
     """Value proto -> flattened scalars of `vt`."""
     d = wire.decode(data)
@@ -240,33 +245,39 @@ class DistributedPointFunction:
 
     def evaluate_until(self, hierarchy_level: int, prefixes: Sequence[int],
                        ctx: EvaluationContext, value_type: ValueType = None,
-                       raw: bool = False):
+                       raw: bool = False, out=None):
         """EvaluateUntil<T> (h:319-322).  Returns decoded values, or the
-        host-layout numpy array with raw=True."""
+        host-layout numpy array with raw=True.  With `out` a torch GPU uint8
+        tensor, the host-layout outputs stay in HBM (written into `out`,
+        dpf_amd_evaluate_until_device) and `out` is returned."""
         vt = self._type(hierarchy_level, value_type)
         tp = vt.to_proto()
-        pw = u128_words(list(prefixes)) if len(prefixes) else np.zeros(2, np.uint64)
+        pw = u128_words(_seq(prefixes)) if len(prefixes) else np.zeros(2, np.uint64)
         n = ctypes.c_int64()
         L = _lib.lib()
-        check(L.dpf_amd_evaluate_until(self._h, hierarchy_level,
-                                       pw.ctypes.data_as(ctypes.c_void_p), len(prefixes),
-                                       tp, len(tp), ctx._h, None, 0, ctypes.byref(n)))
-        out = np.zeros(max(n.value, 1), dtype=vt.numpy_dtype())
-        check(L.dpf_amd_evaluate_until(self._h, hierarchy_level,
-                                       pw.ctypes.data_as(ctypes.c_void_p), len(prefixes),
-                                       tp, len(tp), ctx._h,
-                                       out.ctypes.data_as(ctypes.c_void_p),
-                                       out.nbytes, ctypes.byref(n)))
-        out = out[:n.value]
-        return out if raw else vt.decode(out)
+        pp = pw.ctypes.data_as(ctypes.c_void_p)
+        check(L.dpf_amd_evaluate_until(self._h, hierarchy_level, pp, len(prefixes), tp, len(tp),
+                                       ctx._h, None, 0, ctypes.byref(n)))
+        if out is not None:
+            check(L.dpf_amd_evaluate_until_device(
+                self._h, hierarchy_level, pp, len(prefixes), tp, len(tp), ctx._h,
+                ctypes.c_void_p(out.data_ptr()), out.numel() * out.element_size(),
+                ctypes.byref(n), _lib.stream_ptr()))
+            return out
+        host = np.zeros(max(n.value, 1), dtype=vt.numpy_dtype())
+        check(L.dpf_amd_evaluate_until(self._h, hierarchy_level, pp, len(prefixes), tp, len(tp),
+                                       ctx._h, host.ctypes.data_as(ctypes.c_void_p),
+                                       host.nbytes, ctypes.byref(n)))
+        host = host[:n.value]
+        return host if raw else vt.decode(host)
 
     def evaluate_next(self, prefixes: Sequence[int], ctx: EvaluationContext,
-                      value_type: ValueType = None, raw: bool = False):
+                      value_type: ValueType = None, raw: bool = False, out=None):
         """EvaluateNext<T> (h:324-333)."""
         if not len(prefixes):
-            return self.evaluate_until(0, prefixes, ctx, value_type, raw)
+            return self.evaluate_until(0, prefixes, ctx, value_type, raw, out)
         return self.evaluate_until(ctx.previous_hierarchy_level + 1, prefixes, ctx,
-                                   value_type, raw)
+                                   value_type, raw, out)
 
     def evaluate_at(self, key: DpfKey, hierarchy_level: int, points: Sequence[int],
                     value_type: ValueType = None, raw: bool = False):
@@ -274,7 +285,7 @@ class DistributedPointFunction:
         vt = self._type(hierarchy_level, value_type)
         tp = vt.to_proto()
         data = bytes(key)
-        pw = u128_words(list(points)) if len(points) else np.zeros(2, np.uint64)
+        pw = u128_words(_seq(points)) if len(points) else np.zeros(2, np.uint64)
         out = np.zeros(max(len(points), 1), dtype=vt.numpy_dtype())
         check(_lib.lib().dpf_amd_evaluate_at(self._h, data, len(data), hierarchy_level,
                                              pw.ctypes.data_as(ctypes.c_void_p), len(points),
@@ -293,7 +304,7 @@ class DistributedPointFunction:
         lens = (ctypes.c_size_t * max(len(datas), 1))(*[len(d) for d in datas])
         if len(points) != len(keys):
             raise _lib.DpfAmdError(3, "`keys.size()` != `evaluation_points.size()`")
-        pw = u128_words(list(points)) if len(points) else np.zeros(2, np.uint64)
+        pw = u128_words(_seq(points)) if len(points) else np.zeros(2, np.uint64)
         H = len(self.parameters)
         out = np.zeros(max(H * len(keys), 1), dtype=vt.numpy_dtype())
         check(_lib.lib().dpf_amd_evaluate_and_apply(

@@ -319,10 +319,14 @@ UINT8, UINT16, UINT32, UINT64, UINT128 = (Integer(8), Integer(16), Integer(32),
                                           Integer(64), Integer(128))
 
 
-def u128_words(values: Sequence[int]) -> np.ndarray:
-    out = np.empty(2 * len(values), dtype=np.uint64)
-    for i, v in enumerate(values):
-        v = int(v)
-        out[2 * i] = v & MASK64
-        out[2 * i + 1] = (v >> 64) & MASK64
-    return out
+def u128_words(values) -> np.ndarray:
+    """128-bit values -> flat {lo, hi} uint64 words.  Accepts a sequence of
+    Python ints or an (n, 2) uint64 array of {lo, hi} rows (passed through)."""
+    if isinstance(values, np.ndarray):
+        if values.dtype != np.uint64 or values.ndim != 2 or values.shape[1] != 2:
+            raise ValueError("128-bit arrays must be (n, 2) uint64 {lo, hi} rows")
+        return np.ascontiguousarray(values).reshape(-1)
+    lo = np.fromiter((int(v) & MASK64 for v in values), dtype=np.uint64, count=len(values))
+    hi = np.fromiter(((int(v) >> 64) & MASK64 for v in values), dtype=np.uint64,
+                     count=len(values))
+    return np.stack([lo, hi], axis=1).reshape(-1)

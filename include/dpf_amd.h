@@ -260,6 +260,17 @@ int dpf_amd_evaluate_until(const dpf_amd_dpf* dpf, int hierarchy_level,
                            dpf_amd_ctx* ctx, void* out, int64_t out_capacity,
                            int64_t* num_outputs);
 
+/* As dpf_amd_evaluate_until, with the outputs left in device memory
+ * (`out_device`, HBM) and the work ordered on `stream` (NULL = the calling
+ * thread's stream): the MI355X consumer path — no PCIe copy of the
+ * outputs.  Returns after the outputs are complete. */
+int dpf_amd_evaluate_until_device(const dpf_amd_dpf* dpf, int hierarchy_level,
+                                  const uint64_t* prefixes, int64_t num_prefixes,
+                                  const uint8_t* value_type, size_t value_type_len,
+                                  dpf_amd_ctx* ctx, void* out_device,
+                                  int64_t out_capacity, int64_t* num_outputs,
+                                  void* stream);
+
 /* EvaluateAt<T>(key, level, points) (h:349-354, 913-1070). */
 int dpf_amd_evaluate_at(const dpf_amd_dpf* dpf, const uint8_t* key,
                         size_t key_len, int hierarchy_level,
