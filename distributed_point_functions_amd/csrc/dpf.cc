@@ -1020,28 +1020,53 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
   std::vector<uint128> seeds(n);
   std::vector<uint8_t> cbs(n);
   if (ctx.partial_evaluations_size() > 0 && start_level <= stop_level) {
-    std::unordered_map<uint128, std::pair<uint128, bool>, U128Hash> prev;
-    prev.reserve(ctx.partial_evaluations_size() * 2);
-    for (const PartialEvaluation& e : ctx.partial_evaluations()) {
-      const uint128 prefix = MakeUint128(e.prefix().high(), e.prefix().low());
-      const std::pair<uint128, bool> value{MakeUint128(e.seed().high(), e.seed().low()),
-                                           e.control_bit()};
-      auto it = prev.emplace(prefix, value).first;
-      if (it->second != value)
-        return InvalidArgumentError(
-            "Duplicate prefix in `ctx.partial_evaluations()` with mismatching seed or "
-            "control bit");
-    }
     const int shift = stop_level - start_level;
-    for (int64_t i = 0; i < n; ++i) {
-      const uint128 pp = shift < 128 ? (prefixes[i] >> shift) : 0;
-      auto it = prev.find(pp);
-      if (it == prev.end())
-        return InvalidArgumentError(
-            "Prefix not present in ctx.partial_evaluations at hierarchy level " +
-            std::to_string(hierarchy_level));
-      seeds[i] = it->second.first;
-      cbs[i] = it->second.second ? 1 : 0;
+    const auto& pes = ctx.partial_evaluations();
+    const int64_t m = static_cast<int64_t>(pes.size());
+    auto pe_prefix = [&](int64_t j) {
+      return MakeUint128(pes[j].prefix().high(), pes[j].prefix().low());
+    };
+    auto query = [&](int64_t i) { return shift < 128 ? (prefixes[i] >> shift) : uint128{0}; };
+    // Sorted fast path (the common case: prefixes come from a sorted
+    // candidate list, and the stored evaluations are the previous call's
+    // sorted tree indices): a merge join instead of the reference's btree.
+    bool sorted = true;
+    for (int64_t j = 1; j < m && sorted; ++j) sorted = pe_prefix(j - 1) < pe_prefix(j);
+    for (int64_t i = 1; i < n && sorted; ++i) sorted = query(i - 1) <= query(i);
+    if (sorted) {
+      int64_t j = 0;
+      for (int64_t i = 0; i < n; ++i) {
+        const uint128 pp = query(i);
+        while (j < m && pe_prefix(j) < pp) ++j;
+        if (j == m || pe_prefix(j) != pp)
+          return InvalidArgumentError(
+              "Prefix not present in ctx.partial_evaluations at hierarchy level " +
+              std::to_string(hierarchy_level));
+        seeds[i] = MakeUint128(pes[j].seed().high(), pes[j].seed().low());
+        cbs[i] = pes[j].control_bit() ? 1 : 0;
+      }
+    } else {
+      std::unordered_map<uint128, std::pair<uint128, bool>, U128Hash> prev;
+      prev.reserve(m * 2);
+      for (const PartialEvaluation& e : pes) {
+        const uint128 prefix = MakeUint128(e.prefix().high(), e.prefix().low());
+        const std::pair<uint128, bool> value{MakeUint128(e.seed().high(), e.seed().low()),
+                                             e.control_bit()};
+        auto it = prev.emplace(prefix, value).first;
+        if (it->second != value)
+          return InvalidArgumentError(
+              "Duplicate prefix in `ctx.partial_evaluations()` with mismatching seed or "
+              "control bit");
+      }
+      for (int64_t i = 0; i < n; ++i) {
+        auto it = prev.find(query(i));
+        if (it == prev.end())
+          return InvalidArgumentError(
+              "Prefix not present in ctx.partial_evaluations at hierarchy level " +
+              std::to_string(hierarchy_level));
+        seeds[i] = it->second.first;
+        cbs[i] = it->second.second ? 1 : 0;
+      }
     }
   } else {
     const uint128 seed = MakeUint128(ctx.key().seed().high(), ctx.key().seed().low());
@@ -1135,21 +1160,34 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   DPF_RETURN_IF_ERROR(CorrectionsFor(st, ctx.key(), hierarchy_level, &corr));
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ThreadStream();
 
-  // Unique tree indices in first-appearance order (h:772-796).
+  // Unique tree indices in first-appearance order (h:772-796).  Sorted
+  // prefixes (the usual heavy-hitters candidate list) de-duplicate in one
+  // pass; otherwise a hash map stands in for the reference's btree.
   std::vector<uint128> tree_indices;
   std::vector<std::pair<int64_t, int>> prefix_map;
   if (!prefixes.empty()) {
     const int bbits = st.parameters[prev_h].log_domain_size() - st.hierarchy_to_tree[prev_h];
-    std::unordered_map<uint128, int64_t, U128Hash> inverse;
-    inverse.reserve(num_prefixes * 2);
     tree_indices.reserve(num_prefixes);
     prefix_map.reserve(num_prefixes);
-    for (int64_t i = 0; i < num_prefixes; ++i) {
-      const uint128 ti = prefixes[i] >> bbits;
-      const int bi = static_cast<int>(prefixes[i] & ((uint128{1} << bbits) - 1));
-      auto it = inverse.emplace(ti, static_cast<int64_t>(tree_indices.size()));
-      if (it.second) tree_indices.push_back(ti);
-      prefix_map.emplace_back(it.first->second, bi);
+    bool sorted = true;
+    for (int64_t i = 1; i < num_prefixes && sorted; ++i) sorted = prefixes[i - 1] <= prefixes[i];
+    if (sorted) {
+      for (int64_t i = 0; i < num_prefixes; ++i) {
+        const uint128 ti = prefixes[i] >> bbits;
+        const int bi = static_cast<int>(prefixes[i] & ((uint128{1} << bbits) - 1));
+        if (tree_indices.empty() || tree_indices.back() != ti) tree_indices.push_back(ti);
+        prefix_map.emplace_back(static_cast<int64_t>(tree_indices.size()) - 1, bi);
+      }
+    } else {
+      std::unordered_map<uint128, int64_t, U128Hash> inverse;
+      inverse.reserve(num_prefixes * 2);
+      for (int64_t i = 0; i < num_prefixes; ++i) {
+        const uint128 ti = prefixes[i] >> bbits;
+        const int bi = static_cast<int>(prefixes[i] & ((uint128{1} << bbits) - 1));
+        auto it = inverse.emplace(ti, static_cast<int64_t>(tree_indices.size()));
+        if (it.second) tree_indices.push_back(ti);
+        prefix_map.emplace_back(it.first->second, bi);
+      }
     }
   }
 
