@@ -43,9 +43,12 @@ P64 = 2 ** 64 - 59
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.64 T int32 lane-ops/s
 OPS_PER_AES = 757.5            # bitsliced AES-128 gate count
-LDS_LOOKUPS_PER_AES = 160      # T-table lookups per block (this kernel)
+LDS_LOOKUPS_PER_AES = 160      # T-table lookups per AES block
 LDS_PEAK_LOOKUPS = 256 * 32 * 2.4e9  # ds_read_b32: 32 lane-lookups/clk/CU
 AES_PER_LEAF_C5 = 4.0          # 2(2^32-1) tree + 2 * 2^32 value AES per 2^32 leaves
+# T-table lookups per c5 leaf: 2 x 160 (tree children) + 160 + 133 (the value
+# PRG pair seed, seed + 1 shares 27 lookups of rounds 1-2)
+LDS_LOOKUPS_PER_LEAF_C5 = 613
 
 
 def log(*a):
@@ -256,6 +259,7 @@ def main():
         aes_per_launch = AES_PER_LEAF_C5 * leaves / world  # one launch per rank per step
         aes_s = aes_per_launch / (r["kernel_ms"] / 1e3)
         achieved = aes_s * OPS_PER_AES / 1e12
+        lookups_s = LDS_LOOKUPS_PER_LEAF_C5 * (leaves / world) / (r["kernel_ms"] / 1e3)
         out = {
             "metric": METRIC, "value": value, "unit": "leaves/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
@@ -269,17 +273,19 @@ def main():
                                       (args.log_domain, world)},
             # The T-table AES is bound by LDS lookup issue (ds_read_b32: 32
             # lane-lookups/clk/CU, conflict-free by construction): achieved =
-            # algorithmic AES per launch x 160 lookups / kernel time.
-            "roofline": {"bound": "lds", "achieved": aes_s * LDS_LOOKUPS_PER_AES / 1e12,
+            # leaves per launch x 613 lookups / kernel time (the subtree walk's
+            # extra lookups, ~0.3%, are not counted).
+            "roofline": {"bound": "lds",
+                         "achieved": lookups_s / 1e12,
                          "peak": LDS_PEAK_LOOKUPS / 1e12, "unit": "T lookups/s",
-                         "frac": aes_s * LDS_LOOKUPS_PER_AES / LDS_PEAK_LOOKUPS,
+                         "frac": lookups_s / LDS_PEAK_LOOKUPS,
                          "traffic": traffic_from_profiles("KExpand<8, dpf_amd::EmitU32ModN64>"),
                          "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/)",
                          "algorithmic_bytes": leaves // world * 16,
                          "kernel": "KExpand<8,EmitU32ModN64>", "kernel_ms": r["kernel_ms"],
                          "aes_per_launch": aes_per_launch, "aes_per_leaf": AES_PER_LEAF_C5,
                          "aes_per_s_per_gpu": aes_s,
-                         "lookups_per_aes": LDS_LOOKUPS_PER_AES,
+                         "lookups_per_leaf": LDS_LOOKUPS_PER_LEAF_C5,
                          # implementation-independent view:
                          # a bitsliced AES needs 757.5 gate ops per block
                          "valu_equivalent": {"ops_per_aes": OPS_PER_AES,
@@ -300,9 +306,9 @@ def main():
                 "scaling": "strong",
                 "roofline": {"bound": "hbm", "achieved": scan_gbs, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": scan_gbs / HBM_PEAK_GBS,
-                             "traffic": traffic_from_profiles("KPirScan<1>"),
+                             "traffic": traffic_from_profiles("KPirScanG<1, 4>"),
                              "algorithmic_bytes": pir["per_gpu_bytes"],
-                             "kernel": "KPirScan<1>+KXorFold", "kernel_ms": pir["scan_ms"]},
+                             "kernel": "KPirScanG<1,4>+KXorFold", "kernel_ms": pir["scan_ms"]},
             }
         print(json.dumps(out), flush=True)
     if world > 1:
