@@ -92,6 +92,8 @@ def lib():
          ctypes.POINTER(ValueTypeDesc), P, I32, I32, I64, I64, P, P)
     _sig(L, "dpf_amd_evaluate_points", I32, I64, P, P, P, I32, I32, I64, P, P, P,
          ctypes.POINTER(ValueTypeDesc), P, P, I32, P, P, P, P, P, P)
+    _sig(L, "dpf_amd_dcf_evaluate", I32, I64, P, P, P, P, I32, P, P, P, P,
+         ctypes.POINTER(ValueTypeDesc), P, P, P)
     _sig(L, "dpf_amd_evaluate_points_batched", I32, I64, I64, P, P, P, I32, I32, P, P, P,
          ctypes.POINTER(ValueTypeDesc), P, P, I32, P, P, P, P)
     _sig(L, "dpf_amd_gather_rows", I32, I64, P, I64, I64, P, P, P)
@@ -131,6 +133,11 @@ def _bind_tier2(L):
          ctypes.POINTER(I64), P)
     _sig(L, "dpf_amd_evaluate_at", I32, P, P, SZ, I32, P, I64, P, SZ, P)
     _sig(L, "dpf_amd_evaluate_and_apply", I32, P, P, P, I64, P, I32, P, SZ, P)
+    _sig(L, "dpf_amd_dcf_create", I32, P, SZ, PP)
+    _sig(L, "dpf_amd_dcf_destroy", None, P)
+    _sig(L, "dpf_amd_dcf_generate_keys", I32, P, U64, U64, P, SZ, P, BUF,
+         ctypes.POINTER(SZ), BUF, ctypes.POINTER(SZ))
+    _sig(L, "dpf_amd_dcf_batch_evaluate", I32, P, P, P, I64, P, I64, P, SZ, P)
     _sig(L, "dpf_amd_pir_db_create", I32, PP)
     _sig(L, "dpf_amd_pir_db_insert", I32, P, P, SZ)
     _sig(L, "dpf_amd_pir_db_insert_fixed", I32, P, P, I64, I64)

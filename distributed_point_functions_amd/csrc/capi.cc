@@ -10,6 +10,7 @@
 
 #include "dpf_amd.h"
 #include "dpf_amd/dense_dpf_pir_server.h"
+#include "dpf_amd/distributed_comparison_function.h"
 #include "dpf_amd/distributed_point_function.h"
 #include "internal.h"
 
@@ -20,6 +21,9 @@ struct dpf_amd_dpf {
 };
 struct dpf_amd_ctx {
   EvaluationContext ctx;
+};
+struct dpf_amd_dcf {
+  std::unique_ptr<DistributedComparisonFunction> dcf;
 };
 struct dpf_amd_pir_db {
   std::unique_ptr<DenseDpfPirDatabase::Builder> builder =
@@ -249,6 +253,66 @@ int dpf_amd_evaluate_and_apply(const dpf_amd_dpf* dpf, const uint8_t* const* key
 }
 
 // --- PIR ---------------------------------------------------------------------
+
+// --- DistributedComparisonFunction (dcf/distributed_comparison_function.h) ---
+
+int dpf_amd_dcf_create(const uint8_t* parameters, size_t len, dpf_amd_dcf** out) {
+  DcfParameters p;
+  if (!p.ParseFromArray(parameters, len))
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed DcfParameters proto");
+  StatusOr<std::unique_ptr<DistributedComparisonFunction>> d =
+      DistributedComparisonFunction::Create(p);
+  if (!d.ok()) return Fail(d.status());
+  *out = new dpf_amd_dcf{std::move(*d)};
+  return DPF_AMD_OK;
+}
+
+void dpf_amd_dcf_destroy(dpf_amd_dcf* dcf) { delete dcf; }
+
+int dpf_amd_dcf_generate_keys(dpf_amd_dcf* dcf, uint64_t alpha_lo, uint64_t alpha_hi,
+                              const uint8_t* beta, size_t beta_len, const uint64_t* seeds,
+                              uint8_t** key0, size_t* key0_len, uint8_t** key1,
+                              size_t* key1_len) {
+  Value b;
+  if (!ParseValue(beta, beta_len, &b)) return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed Value proto");
+  const uint128 alpha = MakeUint128(alpha_hi, alpha_lo);
+  StatusOr<std::pair<DcfKey, DcfKey>> keys =
+      seeds ? dcf->dcf->GenerateKeysWithSeeds(alpha, b, MakeUint128(seeds[1], seeds[0]),
+                                              MakeUint128(seeds[3], seeds[2]))
+            : dcf->dcf->GenerateKeys(alpha, b);
+  if (!keys.ok()) return Fail(keys.status());
+  int rc = ToBuffer(keys->first.SerializeAsString(), key0, key0_len);
+  if (rc != DPF_AMD_OK) return rc;
+  rc = ToBuffer(keys->second.SerializeAsString(), key1, key1_len);
+  if (rc != DPF_AMD_OK) free(*key0);
+  return rc;
+}
+
+int dpf_amd_dcf_batch_evaluate(const dpf_amd_dcf* dcf, const uint8_t* const* keys,
+                               const size_t* key_lengths, int64_t num_keys,
+                               const uint64_t* points, int64_t num_points,
+                               const uint8_t* value_type, size_t value_type_len, void* out) {
+  if (num_keys != num_points)
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "`keys` and `evaluation_points` must have the same size");
+  std::vector<DcfKey> ks(num_keys);
+  std::vector<const DcfKey*> ptrs(num_keys);
+  for (int64_t i = 0; i < num_keys; ++i) {
+    if (!ks[i].ParseFromArray(keys[i], key_lengths[i]))
+      return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed DcfKey proto");
+    ptrs[i] = &ks[i];
+  }
+  ValueType t;
+  int rc = ParseType(value_type, value_type_len, &t);
+  if (rc != DPF_AMD_OK) return rc;
+  const DistributedPointFunction& dpf = dcf->dcf->dpf();
+  Status st = dpf.CheckType(t, -1, true);
+  if (!st.ok()) return Fail(st);
+  std::vector<uint128> p = ToU128(points, num_points);
+  st = dcf->dcf->BatchEvaluateRaw(Span<const DcfKey* const>(ptrs.data(), ptrs.size()),
+                                  Span<const uint128>(p.data(), p.size()),
+                                  dpf.value_type_descriptor(dpf.num_hierarchy_levels() - 1), out);
+  return st.ok() ? DPF_AMD_OK : Fail(st);
+}
 
 int dpf_amd_pir_db_create(dpf_amd_pir_db** out) {
   *out = new dpf_amd_pir_db();

@@ -20,6 +20,7 @@
 #include <unordered_map>
 
 #include "host_aes.h"
+#include "host_device.h"
 #include "internal.h"
 
 namespace distributed_point_functions {
@@ -633,62 +634,14 @@ std::string DpfParameters::DebugString() const {
 }
 
 // ---------------------------------------------------------------------------
-// Device helpers
+// Device helpers: csrc/host_device.h
 // ---------------------------------------------------------------------------
+using dpf_internal_host::AbiStatus;
+using dpf_internal_host::DeviceBuffer;
+using dpf_internal_host::HipStatus;
+using dpf_internal_host::ThreadStream;
+
 namespace {
-
-Status HipStatus(hipError_t e, const char* what) {
-  if (e == hipSuccess) return OkStatus();
-  if (e == hipErrorOutOfMemory)
-    return ResourceExhaustedError(std::string(what) + ": " + hipGetErrorString(e));
-  return InternalError(std::string(what) + ": " + hipGetErrorString(e));
-}
-
-Status AbiStatus(int rc) {
-  if (rc == DPF_AMD_OK) return OkStatus();
-  return Status(static_cast<StatusCode>(rc), dpf_amd::LastError());
-}
-
-hipStream_t ThreadStream() {
-  thread_local hipStream_t s = [] {
-    hipStream_t x = nullptr;
-    if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) x = nullptr;
-    return x;
-  }();
-  return s;
-}
-
-class DeviceBuffer {
- public:
-  DeviceBuffer() = default;
-  ~DeviceBuffer() { Reset(); }
-  DeviceBuffer(const DeviceBuffer&) = delete;
-  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
-  Status Alloc(size_t bytes, hipStream_t s) {
-    Reset();
-    stream_ = s;
-    if (bytes == 0) bytes = 16;
-    return HipStatus(hipMallocAsync(&p_, bytes, s), "hipMallocAsync");
-  }
-  Status Upload(const void* src, size_t bytes, hipStream_t s) {
-    DPF_RETURN_IF_ERROR(Alloc(bytes, s));
-    if (bytes == 0) return OkStatus();
-    return HipStatus(hipMemcpyAsync(p_, src, bytes, hipMemcpyHostToDevice, s), "upload");
-  }
-  void Reset() {
-    if (p_) (void)hipFreeAsync(p_, stream_);
-    p_ = nullptr;
-  }
-  void* get() const { return p_; }
-  template <typename T>
-  T* as() const {
-    return static_cast<T*>(p_);
-  }
-
- private:
-  void* p_ = nullptr;
-  hipStream_t stream_ = nullptr;
-};
 
 struct CwArrays {
   std::vector<uint128> seeds;
@@ -993,6 +946,17 @@ Status MergeLayout(const LevelMeta& m, const dpf_amd_value_type& layout, dpf_amd
 }
 
 }  // namespace
+
+Status DistributedPointFunction::ValidateKey(const DpfKey& key) const {
+  return ValidateDpfKey(*state_, key);
+}
+
+Status DistributedPointFunction::ValueCorrectionWords(const DpfKey& key, int level,
+                                                      std::vector<uint128>* out) const {
+  if (level < 0 || level >= num_hierarchy_levels())
+    return InvalidArgumentError("`hierarchy_level` out of range");
+  return CorrectionsFor(*state_, key, level, out);
+}
 
 StatusOr<EvaluationContext> DistributedPointFunction::CreateEvaluationContext(DpfKey key) const {
   DPF_RETURN_IF_ERROR(ValidateDpfKey(*state_, key));

@@ -1,0 +1,72 @@
+// host_device.h — host-side HIP plumbing shared by the Tier-2 objects
+// (csrc/dpf.cc, csrc/dcf.cc): status mapping, the per-thread stream and a
+// stream-ordered device buffer.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "dpf_amd.h"
+#include "dpf_amd/status.h"
+#include "internal.h"
+
+namespace distributed_point_functions {
+namespace dpf_internal_host {
+
+
+inline Status HipStatus(hipError_t e, const char* what) {
+  if (e == hipSuccess) return OkStatus();
+  if (e == hipErrorOutOfMemory)
+    return ResourceExhaustedError(std::string(what) + ": " + hipGetErrorString(e));
+  return InternalError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+inline Status AbiStatus(int rc) {
+  if (rc == DPF_AMD_OK) return OkStatus();
+  return Status(static_cast<StatusCode>(rc), dpf_amd::LastError());
+}
+
+inline hipStream_t ThreadStream() {
+  thread_local hipStream_t s = [] {
+    hipStream_t x = nullptr;
+    if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) x = nullptr;
+    return x;
+  }();
+  return s;
+}
+
+class DeviceBuffer {
+ public:
+  DeviceBuffer() = default;
+  ~DeviceBuffer() { Reset(); }
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+  Status Alloc(size_t bytes, hipStream_t s) {
+    Reset();
+    stream_ = s;
+    if (bytes == 0) bytes = 16;
+    return HipStatus(hipMallocAsync(&p_, bytes, s), "hipMallocAsync");
+  }
+  Status Upload(const void* src, size_t bytes, hipStream_t s) {
+    DPF_RETURN_IF_ERROR(Alloc(bytes, s));
+    if (bytes == 0) return OkStatus();
+    return HipStatus(hipMemcpyAsync(p_, src, bytes, hipMemcpyHostToDevice, s), "upload");
+  }
+  void Reset() {
+    if (p_) (void)hipFreeAsync(p_, stream_);
+    p_ = nullptr;
+  }
+  void* get() const { return p_; }
+  template <typename T>
+  T* as() const {
+    return static_cast<T*>(p_);
+  }
+
+ private:
+  void* p_ = nullptr;
+  hipStream_t stream_ = nullptr;
+};
+
+}  // namespace dpf_internal_host
+}  // namespace distributed_point_functions

@@ -218,6 +218,93 @@ __global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluatePoints(Po
   }
 }
 
+// Threads per block for a walk over n points: full blocks once the launch
+// fills every CU (two blocks each), smaller ones before that so that small
+// launches still spread over all CUs.
+static int WalkBlock(int64_t n) {
+  int64_t per = (n + 2 * 256 - 1) / (2 * 256);
+  per = (per + 63) / 64 * 64;
+  return (int)std::min<int64_t>(kPointsBlock, std::max<int64_t>(64, per));
+}
+
+// Little-endian load of an `nbytes` scalar.
+__device__ __forceinline__ u128 LoadScalar(const char* p, int nbytes) {
+  u128 v = 0;
+  for (int b = nbytes - 1; b >= 0; --b) v = (v << 8) | (uint8_t)p[b];
+  return v;
+}
+
+// Fused DCF BatchEvaluate: one walk per (key i, point i) through all tree
+// levels; at hierarchy level h (log domain h, tree level tree_of[h]) the
+// level's output is needed only when DCF bit (log_domain - h - 1) of the
+// point is 0 (h:150-165 adds it then), so only those levels are hashed,
+// converted, corrected and summed with the value type's + (the skipped
+// levels' outputs are never read, so the result is identical).  Path bit of
+// tree level a: log_domain - 1 - a (EvaluateAndApply rightshift 1).
+template <int BN>
+__global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KDcfEvaluate(DcfArgs a, VtDev vt) {
+  __shared__ uint32_t tab[kTabWords];
+  FillTables(tab);
+  __syncthreads();
+  const Lds L = MakeLds(tab);
+  const int64_t T = (int64_t)gridDim.x * blockDim.x;
+  const int per_elem = vt.epb * vt.ns;
+  const int H = a.log_domain;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += T) {
+    const uint4 s0 = a.seeds[i];
+    uint32_t x[1][4] = {{s0.x, s0.y, s0.z, s0.w}};
+    uint32_t t = a.cb[i];
+    const uint4 p = a.points[i];
+    const u128 pv = (u128)p.x | ((u128)p.y << 32) | ((u128)p.z << 64) | ((u128)p.w << 96);
+    const int party = a.party[i];
+    u128 acc[DPF_AMD_MAX_SCALARS];
+    for (int s = 0; s < vt.ns; ++s) acc[s] = 0;
+    int level = 0;
+    for (int h = 0; h < H; ++h) {
+      const int stop = a.tree_of[h];
+      for (; level < stop; ++level) {
+        const uint32_t bit = PathBit(p, H - 1 - level);
+        const Cw cw = LoadCw(a.cw_seed, a.ccl, a.ccr, (int64_t)level * a.n + i);
+        WalkStep(x[0], t, bit, cw, DpfMasked<1>{{0u - bit}}, L);
+      }
+      if (PathBit(p, H - 1 - h) != 0) continue;
+      u128 W[1][BN];
+      HashSeeds<1, BN>(x, W, L);
+      const int bbits = h - stop;
+      const int e = bbits > 0 ? (int)((pv >> (H - h)) & (((u128)1 << bbits) - 1)) : 0;
+      u128 corr[kMaxCorrections];
+      const uint4* c4 = a.corrections + ((int64_t)h * a.n + i) * per_elem;
+      for (int j = 0; j < per_elem; ++j) {
+        const uint4 c = c4[j];
+        corr[j] = (u128)c.x | ((u128)c.y << 32) | ((u128)c.z << 64) | ((u128)c.w << 96);
+      }
+      alignas(16) char buf[DPF_AMD_MAX_SCALARS * 16];
+      char* dst = buf;
+      EmitLeaf<BN>(vt, W[0], t != 0, party, corr, e, e + 1, [dst](int) { return dst; });
+      for (int s = 0; s < vt.ns; ++s)
+        acc[s] = ScAdd(vt.sc[s], acc[s], LoadScalar(buf + vt.sc[s].out_off, vt.sc[s].bytes));
+    }
+    char* out = a.out + i * (int64_t)vt.stride;
+    for (int s = 0; s < vt.ns; ++s) StoreScalar(out + vt.sc[s].out_off, vt.sc[s].bytes, acc[s]);
+  }
+}
+
+int LaunchDcfEvaluate(int bn, hipStream_t st, const DcfArgs& a, const VtDev& vt) {
+  const int block = WalkBlock(a.n);
+  const int grid = (int)std::min<int64_t>(4 * 256, (a.n + block - 1) / block);
+  switch (bn) {
+    case 1:
+      hipLaunchKernelGGL((KDcfEvaluate<1>), dim3(grid), dim3(block), 0, st, a, vt);
+      break;
+    case 2:
+      hipLaunchKernelGGL((KDcfEvaluate<2>), dim3(grid), dim3(block), 0, st, a, vt);
+      break;
+    default:
+      hipLaunchKernelGGL((KDcfEvaluate<4>), dim3(grid), dim3(block), 0, st, a, vt);
+  }
+  return LaunchCheck("dcf kernel launch");
+}
+
 // Plain AES-MMO hash (Aes128FixedKeyHash::Evaluate).
 __global__ __launch_bounds__(kBlock, 2) void KAesMmo(const uint4* in, uint4* out, int64_t n,
                                                  KeyPair kp) {
@@ -235,15 +322,6 @@ __global__ __launch_bounds__(kBlock, 2) void KAesMmo(const uint4* in, uint4* out
     AesN<1>(st, PairSelect{{}, kp, false}, L);
     out[i] = make_uint4(st[0][0] ^ s[0], st[0][1] ^ s[1], st[0][2] ^ s[2], st[0][3] ^ s[3]);
   }
-}
-
-// Threads per block for a walk over n points: full blocks once the launch
-// fills every CU (two blocks each), smaller ones before that so that small
-// launches still spread over all CUs.
-static int WalkBlock(int64_t n) {
-  int64_t per = (n + 2 * 256 - 1) / (2 * 256);
-  per = (per + 63) / 64 * 64;
-  return (int)std::min<int64_t>(kPointsBlock, std::max<int64_t>(64, per));
 }
 
 int LaunchEvaluateSeeds(int64_t n, hipStream_t st, const WalkArgs& a, const KeyPair& kp) {

@@ -73,6 +73,24 @@ struct PointsArgs {
   char* out;
 };
 
+// KDcfEvaluate (dcf/distributed_comparison_function.h:141-187): key i at
+// point i, hierarchy level h has log domain h (h < log_domain), rightshift 1.
+constexpr int kDcfMaxLevels = 128;
+struct DcfArgs {
+  int64_t n;
+  const uint4* seeds;
+  const uint8_t* cb;
+  const int8_t* party;
+  const uint4* points;
+  const uint4* cw_seed;  // [tree level][key]
+  const uint8_t* ccl;
+  const uint8_t* ccr;
+  const uint4* corrections;  // [hierarchy level][key][epb * ns]
+  char* out;
+  int32_t log_domain;  // DCF log domain = number of hierarchy levels
+  int32_t tree_of[kDcfMaxLevels];  // hierarchy level -> tree level
+};
+
 // KEvaluatePoints: 2 blocks per CU (one 64 KiB table each), 4 waves/SIMD,
 // two points per thread walked in lockstep.
 constexpr int kPointsBlock = 512;
@@ -120,6 +138,7 @@ int LaunchExpandGeneric4(int D, int grid, hipStream_t st, const ExpandArgs& a, c
 int LaunchEvaluateSeeds(int64_t n, hipStream_t st, const WalkArgs& a, const KeyPair& kp);
 int LaunchEvaluatePoints(int bn, int64_t n, hipStream_t st, const PointsArgs& a,
                          const VtDev& vt);
+int LaunchDcfEvaluate(int bn, hipStream_t st, const DcfArgs& a, const VtDev& vt);
 int LaunchAesMmo(int grid, hipStream_t st, const uint4* in, uint4* out, int64_t n,
                  const KeyPair& kp);
 // k_pir.hip

@@ -328,6 +328,39 @@ int dpf_amd_evaluate_points_batched(int64_t num_keys, int64_t points_per_key,
                         stream);
 }
 
+int dpf_amd_dcf_evaluate(int64_t num_keys, const void* seeds, const uint8_t* control_bits,
+                         const int8_t* party, const void* points, int log_domain_size,
+                         const int32_t* tree_level_of, const void* correction_seeds,
+                         const uint8_t* ccl, const uint8_t* ccr, const dpf_amd_value_type* vt,
+                         const void* value_corrections, void* out, void* stream) {
+  if (num_keys < 0 || !vt || !tree_level_of)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "bad arguments");
+  if (log_domain_size < 1 || log_domain_size > kDcfMaxLevels)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "A DCF must have log_domain_size >= 1");
+  for (int h = 0; h < log_domain_size; ++h)
+    if (tree_level_of[h] < 0 || tree_level_of[h] > h ||
+        (h > 0 && tree_level_of[h] < tree_level_of[h - 1]))
+      return SetError(DPF_AMD_INVALID_ARGUMENT, "invalid hierarchy-to-tree map");
+  if (num_keys == 0) return DPF_AMD_OK;
+  VtDev dev;
+  int rc = MakeVtDev(*vt, nullptr, 0, vt->elements_per_block, &dev);
+  if (rc != DPF_AMD_OK) return rc;
+  DcfArgs a;
+  a.n = num_keys;
+  a.seeds = (const uint4*)seeds;
+  a.cb = control_bits;
+  a.party = party;
+  a.points = (const uint4*)points;
+  a.cw_seed = (const uint4*)correction_seeds;
+  a.ccl = ccl;
+  a.ccr = ccr;
+  a.corrections = (const uint4*)value_corrections;
+  a.out = (char*)out;
+  a.log_domain = log_domain_size;
+  for (int h = 0; h < kDcfMaxLevels; ++h) a.tree_of[h] = h < log_domain_size ? tree_level_of[h] : 0;
+  return LaunchDcfEvaluate(BnTemplate(dev.bn), (hipStream_t)stream, a, dev);
+}
+
 int dpf_amd_gather_rows(int64_t num_prefixes, const int64_t* src_offset,
                         int64_t outputs_per_prefix, int64_t stride, const void* in, void* out,
                         void* stream) {

@@ -609,6 +609,46 @@ bool EvaluationContext::ParseFromArray(const void* data, size_t size) {
   return Par(static_cast<const uint8_t*>(data), size, this);
 }
 
+// --- DcfParameters / DcfKey (dcf/distributed_comparison_function.proto) ---
+std::string DcfParameters::SerializeAsString() const {
+  Writer w;
+  if (has_parameters()) w.Message(1, Ser(parameters()));
+  return w.Take();
+}
+bool DcfParameters::ParseFromArray(const void* data, size_t size) {
+  *this = DcfParameters();
+  Reader r(data, size);
+  DPF_FOR_EACH_FIELD(r, f, wt) {
+    const uint8_t* d;
+    size_t l;
+    if (f == 1 && wt == 2) {
+      if (!r.Bytes(&d, &l) || !Par(d, l, mutable_parameters())) return false;
+    } else if (!r.Skip(wt)) {
+      return false;
+    }
+  }
+  return r.ok();
+}
+std::string DcfKey::SerializeAsString() const {
+  Writer w;
+  if (has_key()) w.Message(1, Ser(key()));
+  return w.Take();
+}
+bool DcfKey::ParseFromArray(const void* data, size_t size) {
+  *this = DcfKey();
+  Reader r(data, size);
+  DPF_FOR_EACH_FIELD(r, f, wt) {
+    const uint8_t* d;
+    size_t l;
+    if (f == 1 && wt == 2) {
+      if (!r.Bytes(&d, &l) || !Par(d, l, mutable_key())) return false;
+    } else if (!r.Skip(wt)) {
+      return false;
+    }
+  }
+  return r.ok();
+}
+
 std::string PirConfig::SerializeAsString() const {
   Writer w;
   if (case_ == kDenseDpfPirConfig) {

@@ -166,6 +166,27 @@ int dpf_amd_evaluate_points_batched(
     const void* key_value_corrections, const uint64_t* value_correction_all,
     void* out, void* stream);
 
+/* Fused DistributedComparisonFunction::BatchEvaluate
+ * (dcf/distributed_comparison_function.h:141-187 over EvaluateAndApply
+ * h:1072-1198 with rightshift 1): key i (seed, control bit, party) is
+ * evaluated at points[i] through hierarchy levels h < log_domain_size (log
+ * domain h, tree level tree_level_of[h], a host array); the outputs of the
+ * levels whose DCF bit (log_domain_size - h - 1) of points[i] is 0 are
+ * summed with the value type's + into out[i] (host layout).  Device arrays:
+ * correction words [tree level][key] (tree_level_of[log_domain_size-1]
+ * levels), value corrections [level][key][epb * num_scalars] 128-bit words.
+ * `vt` describes the DCF's value type (same at every level). */
+int dpf_amd_dcf_evaluate(int64_t num_keys, const void* seeds,
+                         const uint8_t* control_bits, const int8_t* party,
+                         const void* points, int log_domain_size,
+                         const int32_t* tree_level_of,
+                         const void* correction_seeds,
+                         const uint8_t* correction_controls_left,
+                         const uint8_t* correction_controls_right,
+                         const dpf_amd_value_type* vt,
+                         const void* value_corrections, void* out,
+                         void* stream);
+
 /* Gathers the per-prefix output slices of an incremental evaluation
  * (h:877-889): out[i * opp + k] = in[src_offset[i] + k] for k < opp, rows of
  * `stride` bytes. */
@@ -285,6 +306,26 @@ int dpf_amd_evaluate_and_apply(const dpf_amd_dpf* dpf,
                                const uint8_t* const* keys,
                                const size_t* key_lengths, int64_t num_keys,
                                const uint64_t* points, int rightshift,
+                               const uint8_t* value_type,
+                               size_t value_type_len, void* out);
+
+/* DistributedComparisonFunction (dcf/distributed_comparison_function.h:30-
+ * 187).  Parameters and keys cross as DcfParameters / DcfKey protos; beta as
+ * a Value proto; `seeds` (4 words: seed0 lo, hi, seed1 lo, hi) replaces the
+ * CSPRNG for fixtures, NULL = CSPRNG.  BatchEvaluate writes num_keys
+ * host-layout T values (T = `value_type`, the DCF's value type). */
+typedef struct dpf_amd_dcf dpf_amd_dcf;
+int dpf_amd_dcf_create(const uint8_t* parameters, size_t len, dpf_amd_dcf** out);
+void dpf_amd_dcf_destroy(dpf_amd_dcf* dcf);
+int dpf_amd_dcf_generate_keys(dpf_amd_dcf* dcf, uint64_t alpha_lo,
+                              uint64_t alpha_hi, const uint8_t* beta,
+                              size_t beta_len, const uint64_t* seeds,
+                              uint8_t** key0, size_t* key0_len,
+                              uint8_t** key1, size_t* key1_len);
+int dpf_amd_dcf_batch_evaluate(const dpf_amd_dcf* dcf,
+                               const uint8_t* const* keys,
+                               const size_t* key_lengths, int64_t num_keys,
+                               const uint64_t* points, int64_t num_points,
                                const uint8_t* value_type,
                                size_t value_type_len, void* out);
 

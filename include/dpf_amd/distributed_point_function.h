@@ -198,6 +198,11 @@ class DistributedPointFunction {
   Status EvaluateAndApplyRaw(Span<const DpfKey* const> keys,
                              Span<const uint128> evaluation_points, int rightshift,
                              const dpf_amd_value_type& vt, void* out, int* levels_done) const;
+  // ProtoValidator::ValidateDpfKey (proto_validator.cc:205-236).
+  Status ValidateKey(const DpfKey& key) const;
+  // The value correction of `key` at hierarchy `level` as flattened 128-bit
+  // scalar words, epb * num_scalars of them (ValuesToArray, vth:561-580).
+  Status ValueCorrectionWords(const DpfKey& key, int level, std::vector<uint128>* out) const;
   // Checks that `type` equals the parameters' type at `level` (all levels if
   // level < 0) (h:709-716).
   Status CheckType(const ValueType& type, int level, bool at) const;

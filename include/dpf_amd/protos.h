@@ -260,6 +260,31 @@ class EvaluationContext {
   int32_t partial_evaluations_level_ = 0;
 };
 
+// --- DCF messages (dcf/distributed_comparison_function.proto:25-32) --------
+
+class DcfParameters {
+ public:
+  DPF_AMD_MESSAGE_FIELD(DpfParameters, parameters)
+  std::string SerializeAsString() const;
+  bool ParseFromArray(const void* data, size_t size);
+
+ private:
+  bool has_parameters_ = false;
+  DpfParameters parameters_;
+};
+
+class DcfKey {
+ public:
+  DPF_AMD_MESSAGE_FIELD(DpfKey, key)
+  std::string SerializeAsString() const;
+  bool ParseFromString(const std::string& data) { return ParseFromArray(data.data(), data.size()); }
+  bool ParseFromArray(const void* data, size_t size);
+
+ private:
+  bool has_key_ = false;
+  DpfKey key_;
+};
+
 // --- PIR messages (pir/private_information_retrieval.proto) ---------------
 
 class DenseDpfPirConfig {
