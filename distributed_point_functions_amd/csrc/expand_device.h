@@ -11,6 +11,10 @@
 #endif
 #include "aes_device.h"
 
+#ifndef DPF_EXPAND_MAX_GRID
+#define DPF_EXPAND_MAX_GRID (1 << 24)
+#endif
+
 namespace dpf_amd {
 
 template <int BN>
@@ -287,6 +291,11 @@ __global__ __launch_bounds__(kExpandBlock, kExpandWaves) void KExpand(ExpandArgs
 
 template <int D, class Em>
 int LaunchExpand(int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
+  // One subtree per thread, many more blocks than resident slots: blocks
+  // finish at different times (per-CU clocks differ) and the dispatcher
+  // back-fills.  c5: 2^24 subtrees / 768 = 21845 blocks -> 166.8 ms, vs
+  // 173.8 ms capped at 2730 blocks and 180.5 ms at one resident round.
+  grid = std::min(grid, DPF_EXPAND_MAX_GRID);
   hipLaunchKernelGGL((KExpand<D, Em>), dim3(grid), dim3(kExpandBlock), 0, st, a, vt);
   return LaunchCheck("expand kernel launch");
 }

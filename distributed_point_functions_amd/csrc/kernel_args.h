@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
 
 #include "aes_tables.h"
@@ -93,8 +94,12 @@ struct DcfArgs {
 
 // KEvaluatePoints: 2 blocks per CU (one 64 KiB table each), 4 waves/SIMD,
 // two points per thread walked in lockstep.
-constexpr int kPointsBlock = 512;
-constexpr int kPointsWaves = 4;
+#ifndef DPF_POINTS_BLOCK
+#define DPF_POINTS_BLOCK 512
+#define DPF_POINTS_WAVES 4
+#endif
+constexpr int kPointsBlock = DPF_POINTS_BLOCK;
+constexpr int kPointsWaves = DPF_POINTS_WAVES;
 
 constexpr int kScanBlock = 256;
 constexpr int kScanWaves = kScanBlock / 64;
@@ -122,6 +127,7 @@ inline int HipCheck(hipError_t e, const char* what) {
 }
 
 inline int LaunchCheck(const char* what) { return HipCheck(hipGetLastError(), what); }
+
 
 // k_expand_*.hip: fused expansion with DFS depth D in {0,1,2,4,8}.
 int LaunchExpandU32ModN64(int D, int grid, hipStream_t st, const ExpandArgs& a,

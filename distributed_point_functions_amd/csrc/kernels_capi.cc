@@ -247,7 +247,8 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
   a.chunk_end = (leaf_end + (1ll << D) - 1) >> D;
   a.leaf_begin = leaf_begin;
   a.leaf_end = leaf_end;
-  const int grid = GridFor(a.chunk_end - a.chunk_begin, kExpandBlock, 8192 * 256 / kExpandBlock);
+  // LaunchExpand caps the grid (DPF_EXPAND_MAX_GRID).
+  const int grid = GridFor(a.chunk_end - a.chunk_begin, kExpandBlock, INT32_MAX);
   return LaunchExpandForType(D, grid, (hipStream_t)stream, a, dev);
 }
 
@@ -385,16 +386,22 @@ int dpf_amd_xor_fold(const void* parts, int num_parts, int64_t bytes, void* out,
                             bytes, (uint8_t*)out);
 }
 
-static int ScanGrid(int64_t num_records) {
-  // ~8 resident 256-thread blocks per CU on 256 CUs; at least one tile per wave.
+static int ScanGrid(int64_t num_records, int num_queries, int64_t record_stride) {
+  // At least one 128-record tile per wave; up to 8192 blocks (c4 Q = 8:
+  // 2.95 ms vs 3.17 ms at 2048 — more, shorter blocks balance across CUs),
+  // but at most 64 MiB of partials (grid x queries x record bytes) for the
+  // fold, and never fewer than 2048 blocks.
   const int64_t tiles = (num_records + 127) / 128;
-  int64_t g = (tiles + kScanWaves - 1) / kScanWaves;
-  return (int)std::max<int64_t>(1, std::min<int64_t>(g, 2048));
+  const int64_t g = (tiles + kScanWaves - 1) / kScanWaves;
+  const int64_t per_block = std::max<int64_t>(1, (int64_t)num_queries * record_stride);
+  const int64_t cap = std::max<int64_t>(2048, std::min<int64_t>(8192, (64ll << 20) / per_block));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
 }
 
 int64_t dpf_amd_inner_product_workspace_size(int64_t num_records, int64_t record_stride,
                                              int num_queries) {
-  return (int64_t)ScanGrid(num_records) * num_queries * record_stride;
+  return (int64_t)ScanGrid(num_records, num_queries, record_stride) * num_queries *
+         record_stride;
 }
 
 int dpf_amd_inner_product(const void* db, int64_t num_records, int64_t record_stride,
@@ -411,8 +418,9 @@ int dpf_amd_inner_product(const void* db, int64_t num_records, int64_t record_st
                         std::to_string(selection_blocks * 128) +
                         ", expected: " + std::to_string(num_records));
   hipStream_t st = (hipStream_t)stream;
-  const int grid = ScanGrid(num_records);
   const int C = (int)(record_stride / 16);
+  const int per_pass = PirScanQueries(C);
+  const int grid = ScanGrid(num_records, num_queries, record_stride);
   ScanArgs a;
   a.db = (const uint4*)db;
   a.sel = (const uint4*)selections;
@@ -422,7 +430,6 @@ int dpf_amd_inner_product(const void* db, int64_t num_records, int64_t record_st
   a.C = C;
   a.total_q = num_queries;
   const dim3 g(grid, (C + 63) / 64);
-  const int per_pass = PirScanQueries(C);
   for (int q0 = 0; q0 < num_queries; q0 += per_pass) {
     const int nq = std::min(per_pass, num_queries - q0);
     a.q0 = q0;
