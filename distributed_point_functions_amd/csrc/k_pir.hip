@@ -21,6 +21,39 @@ __global__ void KGatherRows(int64_t n, const int64_t* src_offset, int64_t opp,
   }
 }
 
+// 16-byte variant: every segment (opp x stride bytes) is a whole number of
+// 16-byte words at a 16-byte-aligned source offset.
+__global__ void KGatherRows16(int64_t n, const int64_t* src_offset, int64_t seg_words,
+                              int64_t src_words_per_unit, const uint4* in, uint4* out) {
+  const int64_t total = n * seg_words;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total; w += step) {
+    const int64_t i = w / seg_words, k = w - i * seg_words;
+    out[w] = in[src_offset[i] * src_words_per_unit + k];
+  }
+}
+
+// As KGatherRows16 for strides that divide 16 (1, 2, 4, 8-byte rows):
+// source row r starts word r / rows_per_word when r is a multiple of
+// rows_per_word (EvaluateUntil's offsets are multiples of opp); other
+// segments are copied byte-wise.
+__global__ void KGatherRowsSmall(int64_t n, const int64_t* src_offset, int64_t seg_words,
+                                 int64_t rows_per_word, const uint4* in, uint4* out) {
+  const int64_t total = n * seg_words;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total; w += step) {
+    const int64_t i = w / seg_words, k = w - i * seg_words;
+    const int64_t r = src_offset[i];
+    if (r % rows_per_word == 0) {
+      out[w] = in[r / rows_per_word + k];
+    } else {
+      const uint8_t* src = reinterpret_cast<const uint8_t*>(in) + r * (16 / rows_per_word) + 16 * k;
+      uint8_t* dst = reinterpret_cast<uint8_t*>(out + w);
+      for (int b = 0; b < 16; ++b) dst[b] = src[b];
+    }
+  }
+}
+
 // XOR of num_parts equally sized partial vectors.  A 256-thread block owns
 // kFoldWords consecutive 16-byte words; its threads split the parts into
 // kFoldSlices interleaved slices (loads of one part stay contiguous), then the
@@ -232,8 +265,20 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
 
 int LaunchGatherRows(int grid, hipStream_t st, int64_t n, const int64_t* src_offset,
                      int64_t opp, int64_t stride, const char* in, char* out) {
-  hipLaunchKernelGGL(KGatherRows, dim3(grid), dim3(256), 0, st, n, src_offset, opp, stride,
-                     in, out);
+  // Row offsets are multiples of opp rows; with (opp x stride) % 16 == 0 and
+  // 16-byte-aligned buffers every segment is whole 16-byte words.
+  if ((opp * stride) % 16 == 0 && (uintptr_t)in % 16 == 0 && (uintptr_t)out % 16 == 0 &&
+      (opp * stride) / 16 > 0 && stride % 16 == 0) {
+    hipLaunchKernelGGL(KGatherRows16, dim3(grid), dim3(256), 0, st, n, src_offset,
+                       opp * stride / 16, stride / 16, (const uint4*)in, (uint4*)out);
+  } else if ((opp * stride) % 16 == 0 && (uintptr_t)in % 16 == 0 && (uintptr_t)out % 16 == 0 &&
+             (16 % stride) == 0) {
+    hipLaunchKernelGGL(KGatherRowsSmall, dim3(grid), dim3(256), 0, st, n, src_offset,
+                       opp * stride / 16, 16 / stride, (const uint4*)in, (uint4*)out);
+  } else {
+    hipLaunchKernelGGL(KGatherRows, dim3(grid), dim3(256), 0, st, n, src_offset, opp, stride,
+                       in, out);
+  }
   return LaunchCheck("gather kernel launch");
 }
 

@@ -153,6 +153,18 @@ def inner_product(db: torch.Tensor, num_records: int, record_stride: int,
     return out
 
 
+def gather_rows(src_offset: torch.Tensor, outputs_per_prefix: int, stride: int,
+                rows: torch.Tensor, out: torch.Tensor = None):
+    """out[i * opp + k] = rows[src_offset[i] + k] for rows of `stride` bytes
+    (dpf_amd_gather_rows, the per-prefix slices of EvaluateUntil h:877-889)."""
+    n = src_offset.numel()
+    if out is None:
+        out = torch.empty(n * outputs_per_prefix * stride, dtype=torch.uint8, device=rows.device)
+    check(_lib.lib().dpf_amd_gather_rows(n, dptr(src_offset), outputs_per_prefix, stride,
+                                         dptr(rows), dptr(out), stream_ptr()))
+    return out
+
+
 def xor_fold(parts: torch.Tensor, num_parts: int, nbytes: int, out=None):
     if out is None:
         out = torch.empty(nbytes, dtype=torch.uint8, device=parts.device)

@@ -284,6 +284,25 @@ def test_evaluate_points_batched_matches_oracle(K, cuda, spec, ld, nkeys, ppk):
         assert [got[k * ppk + j] for j in sample] == want, k
 
 
+@pytest.mark.parametrize("stride,opp", [(1, 32), (2, 8), (4, 4), (8, 256), (8, 3), (16, 5),
+                                        (24, 7), (32, 64), (12, 4)])
+def test_gather_rows(K, cuda, stride, opp):
+    """Per-prefix slice gather (h:877-889) on 16-byte and byte paths, with
+    aligned and unaligned row offsets."""
+    import torch
+    rng = np.random.default_rng(stride * 100 + opp)
+    total_rows = 4096
+    rows = rng.integers(0, 256, size=total_rows * stride, dtype=np.uint8)
+    n = 300
+    src = rng.integers(0, total_rows - opp, size=n).astype(np.int64)
+    src[::3] = (src[::3] // opp) * opp  # EvaluateUntil's offsets are multiples of opp
+    got = K.gather_rows(torch.from_numpy(src).to(cuda), opp, stride,
+                        torch.from_numpy(rows).to(cuda)).cpu().numpy()
+    r2 = rows.reshape(total_rows, stride)
+    want = np.concatenate([r2[s:s + opp].reshape(-1) for s in src])
+    assert np.array_equal(got, want)
+
+
 # ---------------------------------------------------------------------------
 # Dense PIR scan vs oracle InnerProduct
 # ---------------------------------------------------------------------------
