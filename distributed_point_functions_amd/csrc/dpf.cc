@@ -639,6 +639,7 @@ std::string DpfParameters::DebugString() const {
 using dpf_internal_host::AbiStatus;
 using dpf_internal_host::DeviceBuffer;
 using dpf_internal_host::HipStatus;
+using dpf_internal_host::HostTrace;
 using dpf_internal_host::ThreadStream;
 
 namespace {
@@ -978,6 +979,7 @@ namespace {
 Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixes,
                                  int hierarchy_level, bool update_ctx, EvaluationContext& ctx,
                                  hipStream_t s, DeviceBuffer* seeds_dev, DeviceBuffer* cb_dev) {
+  HostTrace trace("PartialEvaluations");
   const int64_t n = static_cast<int64_t>(prefixes.size());
   int start_level = st.hierarchy_to_tree[ctx.partial_evaluations_level()];
   const int stop_level = st.hierarchy_to_tree[hierarchy_level];
@@ -1038,6 +1040,7 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
     std::fill(cbs.begin(), cbs.end(), static_cast<uint8_t>(ctx.key().party() != 0));
     start_level = 0;
   }
+  trace.Mark("lookup");
   const int levels = stop_level - start_level;
   CwArrays cw = KeyCws(ctx.key(), start_level, stop_level);
   DeviceBuffer paths, cws, ccl, ccr;
@@ -1054,6 +1057,7 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
         dpf_amd::kPrgKeyRightLo, dpf_amd::kPrgKeyRightHi, seeds_dev->get(),
         cb_dev->as<uint8_t>(), s)));
   }
+  trace.Mark("upload+walk_launch");
   ctx.clear_partial_evaluations();
   if (update_ctx && n > 0) {
     DPF_RETURN_IF_ERROR(HipStatus(
@@ -1072,6 +1076,7 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
       e.set_control_bit(cbs[i] != 0);
     }
   }
+  trace.Mark("d2h+ctx_rewrite");
   ctx.set_partial_evaluations_level(hierarchy_level);
   return OkStatus();
 }
@@ -1085,7 +1090,9 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
                                                   int64_t out_capacity, int64_t* num_outputs,
                                                   bool out_on_device, void* stream) const {
   const DpfState& st = *state_;
+  HostTrace trace("EvaluateUntil");
   DPF_RETURN_IF_ERROR(ValidateEvaluationContext(st, ctx));
+  trace.Mark("validate_ctx");
   const int L = num_hierarchy_levels();
   if (hierarchy_level < 0 || hierarchy_level >= L)
     return InvalidArgumentError(
@@ -1155,6 +1162,7 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
     }
   }
 
+  trace.Mark("checks+dedup");
   // ExpandAndUpdateContext (cc:478-521): roots on the device.
   DeviceBuffer root_seeds, root_cb;
   int start_level = 0;
@@ -1170,6 +1178,7 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
         ctx, s, &root_seeds, &root_cb));
     start_level = st.hierarchy_to_tree[prev_h];
   }
+  trace.Mark("partial_evaluations");
   const int stop_level = st.hierarchy_to_tree[hierarchy_level];
   const int levels = stop_level - start_level;
   CwArrays cw = KeyCws(ctx.key(), start_level, stop_level);
@@ -1195,6 +1204,7 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
       ccr.as<uint8_t>(), &vt, reinterpret_cast<const uint64_t*>(corr.data()),
       ctx.key().party(), cepb, 0, num_roots << levels, expand_out, s)));
 
+  trace.Mark("expand_launch");
   void* final_dev = expand_out;
   if (!prefixes.empty()) {
     // Per-prefix slices (h:877-889).
@@ -1219,6 +1229,7 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
     DPF_RETURN_IF_ERROR(HipStatus(
         hipMemcpyAsync(out, final_dev, total * stride, hipMemcpyDeviceToHost, s), "d2h"));
   DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+  trace.Mark("gather+copy+sync");
   ctx.set_previous_hierarchy_level(hierarchy_level);
   return OkStatus();
 }

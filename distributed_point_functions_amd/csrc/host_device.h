@@ -5,6 +5,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "dpf_amd.h"
@@ -35,6 +38,28 @@ inline hipStream_t ThreadStream() {
   }();
   return s;
 }
+
+// Host-side phase timer: with DPF_AMD_TRACE_HOST set, Mark(name) prints the
+// wall time since the previous mark to stderr (the reference has no tracing;
+// this is how the Tier-2 host overhead is attributed).
+class HostTrace {
+ public:
+  explicit HostTrace(const char* scope)
+      : scope_(scope), on_(std::getenv("DPF_AMD_TRACE_HOST") != nullptr),
+        t_(std::chrono::steady_clock::now()) {}
+  void Mark(const char* phase) {
+    if (!on_) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[dpf_amd] %s/%s %.3f ms\n", scope_, phase,
+                 std::chrono::duration<double, std::milli>(now - t_).count());
+    t_ = now;
+  }
+
+ private:
+  const char* scope_;
+  bool on_;
+  std::chrono::steady_clock::time_point t_;
+};
 
 class DeviceBuffer {
  public:
