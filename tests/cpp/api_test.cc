@@ -1,0 +1,142 @@
+// api_test.cc — the reference's C++ API used as a drop-in: this file is
+// written against include/dpf_amd/*.h exactly as a caller of
+// dpf/distributed_point_function.h and dcf/distributed_comparison_function.h
+// would write it (templates, StatusOr, Span), and links libdpf_amd.so.
+// Checks mirror the reference's tests:
+//   distributed_point_function_test.cc:1015-1042 (full-domain share-sum),
+//   :1044-1079 (EvaluateAt share-sum), :652-696 (incremental),
+//   distributed_comparison_function_test.cc:106-133 (GenEval).
+// Exit status 0 = all checks passed.  Built and run by tests/test_cpp_api.py.
+#include <cstdio>
+#include <vector>
+
+#include "dpf_amd/distributed_comparison_function.h"
+#include "dpf_amd/distributed_point_function.h"
+
+using namespace distributed_point_functions;
+
+static int failures = 0;
+#define CHECK(cond)                                                                  \
+  do {                                                                               \
+    if (!(cond)) {                                                                   \
+      std::fprintf(stderr, "%s:%d: CHECK failed: %s\n", __FILE__, __LINE__, #cond); \
+      ++failures;                                                                    \
+    }                                                                                \
+  } while (0)
+#define CHECK_OK(expr)                                                \
+  do {                                                                \
+    if (!(expr).ok()) {                                               \
+      std::fprintf(stderr, "%s:%d: not OK: %s\n", __FILE__, __LINE__, \
+                   (expr).status().ToString().c_str());               \
+      return 1;                                                       \
+    }                                                                 \
+  } while (0)
+
+static int FullDomainUint64() {
+  DpfParameters p;
+  p.set_log_domain_size(10);
+  p.mutable_value_type()->mutable_integer()->set_bitsize(64);
+  auto dpf = DistributedPointFunction::Create(p);
+  CHECK_OK(dpf);
+  const uint128 alpha = 123;
+  auto keys = (*dpf)->GenerateKeys(alpha, uint128{42});
+  CHECK_OK(keys);
+  auto c0 = (*dpf)->CreateEvaluationContext(keys->first);
+  auto c1 = (*dpf)->CreateEvaluationContext(keys->second);
+  CHECK_OK(c0);
+  CHECK_OK(c1);
+  auto r0 = (*dpf)->EvaluateNext<uint64_t>(Span<const uint128>(), *c0);
+  auto r1 = (*dpf)->EvaluateNext<uint64_t>(Span<const uint128>(), *c1);
+  CHECK_OK(r0);
+  CHECK_OK(r1);
+  CHECK(r0->size() == 1024 && r1->size() == 1024);
+  for (size_t x = 0; x < r0->size(); ++x)
+    CHECK(uint64_t((*r0)[x] + (*r1)[x]) == (x == alpha ? 42u : 0u));
+  // EvaluateAt on a few points of the same keys.
+  std::vector<uint128> pts = {0, 122, 123, 124, 1023};
+  auto a0 = (*dpf)->EvaluateAt<uint64_t>(keys->first, 0, pts);
+  auto a1 = (*dpf)->EvaluateAt<uint64_t>(keys->second, 0, pts);
+  CHECK_OK(a0);
+  CHECK_OK(a1);
+  for (size_t i = 0; i < pts.size(); ++i)
+    CHECK(uint64_t((*a0)[i] + (*a1)[i]) == (pts[i] == alpha ? 42u : 0u));
+  return 0;
+}
+
+using P64 = IntModN<uint64_t, 18446744073709551557ull>;
+using C5 = Tuple<uint32_t, P64>;
+
+static int IncrementalTuple() {
+  // Two hierarchy levels of the c5 value type (security_parameter = 48).
+  std::vector<DpfParameters> ps(2);
+  ps[0].set_log_domain_size(6);
+  ps[1].set_log_domain_size(12);
+  for (auto& p : ps) {
+    *p.mutable_value_type() = ToValueType<C5>();
+    p.set_security_parameter(48);
+  }
+  auto dpf = DistributedPointFunction::CreateIncremental(ps);
+  CHECK_OK(dpf);
+  const uint128 alpha = 0xabc;
+  std::vector<C5> betas = {C5(7u, P64(11)), C5(13u, P64(17))};
+  auto keys = (*dpf)->GenerateKeysIncremental<C5>(alpha, Span<const C5>(betas.data(), 2));
+  CHECK_OK(keys);
+  auto c0 = (*dpf)->CreateEvaluationContext(keys->first);
+  auto c1 = (*dpf)->CreateEvaluationContext(keys->second);
+  CHECK_OK(c0);
+  CHECK_OK(c1);
+  auto l0a = (*dpf)->EvaluateNext<C5>(Span<const uint128>(), *c0);
+  auto l0b = (*dpf)->EvaluateNext<C5>(Span<const uint128>(), *c1);
+  CHECK_OK(l0a);
+  CHECK_OK(l0b);
+  for (size_t x = 0; x < 64; ++x)
+    CHECK(((*l0a)[x] + (*l0b)[x]) == ((x == (alpha >> 6)) ? betas[0] : C5()));
+  std::vector<uint128> prefixes = {1, alpha >> 6, 60};
+  auto l1a = (*dpf)->EvaluateNext<C5>(prefixes, *c0);
+  auto l1b = (*dpf)->EvaluateNext<C5>(prefixes, *c1);
+  CHECK_OK(l1a);
+  CHECK_OK(l1b);
+  CHECK(l1a->size() == 3 * 64);
+  for (size_t i = 0; i < l1a->size(); ++i) {
+    const uint128 x = (prefixes[i / 64] << 6) | (i % 64);
+    CHECK(((*l1a)[i] + (*l1b)[i]) == (x == alpha ? betas[1] : C5()));
+  }
+  return 0;
+}
+
+static int DcfGenEval() {
+  DcfParameters p;
+  p.mutable_parameters()->set_log_domain_size(5);
+  p.mutable_parameters()->mutable_value_type()->mutable_integer()->set_bitsize(32);
+  auto dcf = DistributedComparisonFunction::Create(p);
+  CHECK_OK(dcf);
+  for (uint128 alpha = 0; alpha < 32; alpha += 5) {
+    auto keys = (*dcf)->GenerateKeys<uint32_t>(alpha, 42u);
+    CHECK_OK(keys);
+    std::vector<DcfKey> k0(32, keys->first), k1(32, keys->second);
+    std::vector<uint128> xs(32);
+    for (int x = 0; x < 32; ++x) xs[x] = x;
+    auto r0 = (*dcf)->BatchEvaluate<uint32_t>(k0, xs);
+    auto r1 = (*dcf)->BatchEvaluate<uint32_t>(k1, xs);
+    CHECK_OK(r0);
+    CHECK_OK(r1);
+    for (int x = 0; x < 32; ++x)
+      CHECK(uint32_t((*r0)[x] + (*r1)[x]) == (uint128(x) < alpha ? 42u : 0u));
+  }
+  // Error path with the reference's message.
+  DcfParameters bad;
+  bad.mutable_parameters()->set_log_domain_size(0);
+  auto e = DistributedComparisonFunction::Create(bad);
+  CHECK(!e.ok() && e.status().message() == "A DCF must have log_domain_size >= 1");
+  return 0;
+}
+
+int main() {
+  if (FullDomainUint64() || IncrementalTuple() || DcfGenEval()) return 2;
+  if (failures) {
+    std::fprintf(stderr, "%d check(s) failed\n", failures);
+    return 1;
+  }
+  std::printf("cpp api: all checks passed\n");
+  return 0;
+}

@@ -1,0 +1,29 @@
+"""The reference's C++ API as a drop-in (tests/cpp/api_test.cc): a plain g++
+program written against include/dpf_amd/*.h — DistributedPointFunction
+(Create / GenerateKeys / CreateEvaluationContext / EvaluateNext / EvaluateAt,
+incremental Tuple<uint32, IntModN<uint64, p>>) and
+DistributedComparisonFunction (GenerateKeys / BatchEvaluate) with the
+reference tests' share-sum checks — linked against libdpf_amd.so.
+Built by build_native; CPU: it exists and resolves every symbol; GPU: it
+runs and passes."""
+import os
+import subprocess
+
+import pytest
+
+from distributed_point_functions_amd import build_native
+
+
+def test_cpp_api_program_is_built_and_links():
+    assert os.path.exists(build_native.CPP_TEST), "run build_native first"
+    out = subprocess.run(["ldd", "-r", build_native.CPP_TEST], capture_output=True, text=True)
+    assert "libdpf_amd.so" in out.stdout
+    assert "undefined symbol" not in out.stdout + out.stderr
+    assert "not found" not in out.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_api_program_runs(cuda):
+    r = subprocess.run([build_native.CPP_TEST], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "all checks passed" in r.stdout
