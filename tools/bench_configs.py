@@ -11,6 +11,9 @@ c3  incremental heavy hitters: 16 levels 8,16,..,128 bits, uint64, 2^16
     surviving prefixes per level (generator of distributed_point_function_
     benchmark.cc:154-191, distinct prefixes); Tier-2 EvaluateNext per level
 c4q dense-PIR XOR scan at Q = 8 and 64 over 2^26 x 256 B (kernel only)
+dcf DistributedComparisonFunction BatchEvaluate, log_domain 32, uint64
+    (distributed_comparison_function_benchmark.cc:31-63 shape): 1024 keys
+    via the Tier-2 API, and 2^20 (key, point) pairs through the fused kernel
 
 Kernel times are HIP events on the launch stream; API times are wall clock.
 Every config also checks its outputs (share-sum / reconstruction).
@@ -18,6 +21,7 @@ Every config also checks its outputs (share-sum / reconstruction).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import random
@@ -272,9 +276,81 @@ def c4q(dev, reps):
     return res
 
 
+def dcf(dev, reps):
+    from distributed_point_functions_amd.dcf import DcfParameters, DistributedComparisonFunction
+    rng = random.Random(5)
+    n_log, nkeys = 32, 1024
+    d = DistributedComparisonFunction.create(DcfParameters(DpfParameters(n_log, V.Integer(64))))
+    alphas = [rng.getrandbits(n_log) for _ in range(nkeys)]
+    betas = [rng.getrandbits(64) for _ in range(nkeys)]
+    pairs = [d.generate_keys(a, b, seeds=(2 * i + 7, 2 * i + 8))
+             for i, (a, b) in enumerate(zip(alphas, betas))]
+    k0 = [p[0] for p in pairs]
+    xs = [rng.getrandbits(n_log) for _ in range(nkeys)]
+    t_api = wall_time(lambda: d.batch_evaluate(k0, xs, raw=True), max(1, reps // 2))
+    r0 = d.batch_evaluate(k0, xs)
+    r1 = d.batch_evaluate([p[1] for p in pairs], xs)
+    ok = all((a + b) % (1 << 64) == (beta if x < al else 0)
+             for a, b, x, al, beta in zip(r0, r1, xs, alphas, betas))
+    # Tier 1: 2^20 evaluations, key i % 1024 at random points.
+    H = n_log
+    # the DCF's incremental DPF (log domains 0..n-1) gives the tree levels
+    mirror = DistributedPointFunction.create_incremental(
+        [DpfParameters(h, V.Integer(64)) for h in range(H)])
+    tree_of = np.array([mirror.hierarchy_to_tree(h) for h in range(H)], dtype=np.int32)
+    L = int(tree_of[-1])
+    n = 1 << 20
+    rep = n // nkeys
+    seeds = np.zeros((nkeys, 2), np.uint64)
+    cw = np.zeros((L, nkeys, 2), np.uint64)
+    ccl = np.zeros((L, nkeys), np.uint8)
+    ccr = np.zeros((L, nkeys), np.uint8)
+    epb = 2  # ElementsPerBlock<uint64_t>: one value correction per element
+    corr = np.zeros((H, nkeys, epb, 2), np.uint64)
+    for i, k in enumerate(k0):
+        dk = k.key
+        seeds[i] = (dk.seed & M64, dk.seed >> 64)
+        for a in range(L):
+            c = dk.correction_words[a]
+            cw[a, i] = (c.seed & M64, c.seed >> 64)
+            ccl[a, i], ccr[a, i] = int(c.control_left), int(c.control_right)
+        for h in range(H):
+            vals = (dk.last_level_value_correction if h == H - 1
+                    else dk.correction_words[int(tree_of[h])].value_correction)
+            assert len(vals) == epb
+            for e in range(epb):
+                v = decode_value(V.Integer(64), vals[e])[0]
+                corr[h, i, e] = (v & M64, v >> 64)
+    tile = lambda a, axis: np.ascontiguousarray(np.repeat(a, rep, axis=axis))  # noqa: E731
+    T = lambda a: torch.from_numpy(a.view(np.int64) if a.dtype == np.uint64 else a).to(dev)  # noqa
+    d_seeds = T(tile(seeds, 0))
+    d_cb = torch.zeros(n, dtype=torch.uint8, device=dev)
+    d_party = torch.zeros(n, dtype=torch.int8, device=dev)
+    pts = np.zeros((n, 2), np.uint64)
+    pts[:, 0] = np.frombuffer(np.random.default_rng(6).bytes(8 * n), dtype=np.uint64) >> 32
+    d_pts = T(pts)
+    d_cw, d_ccl, d_ccr = T(tile(cw, 1)), T(tile(ccl, 1)), T(tile(ccr, 1))
+    d_corr = T(tile(corr, 1))
+    out = torch.empty(n * 8, dtype=torch.uint8, device=dev)
+    desc = mirror.value_type_descriptor(H - 1)
+    tree_c = tree_of.ctypes.data_as(ctypes.c_void_p)
+    from distributed_point_functions_amd._lib import check, dptr, stream_ptr
+
+    def run():
+        check(_lib.lib().dpf_amd_dcf_evaluate(
+            n, dptr(d_seeds), dptr(d_cb), dptr(d_party), dptr(d_pts), H, tree_c, dptr(d_cw),
+            dptr(d_ccl), dptr(d_ccr), ctypes.byref(desc), dptr(d_corr), dptr(out),
+            stream_ptr()))
+    t_k = ev_time(run, reps)
+    return {"config": "dcf", "workload": "DCF BatchEvaluate log_domain=32 uint64",
+            "api_keys": nkeys, "api_ms": t_api * 1e3,
+            "kernel_evaluations": n, "kernel_ms": t_k * 1e3,
+            "kernel_evaluations_per_s": n / t_k, "correct": bool(ok)}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="c1,c2,c3,c4q")
+    ap.add_argument("--only", default="c1,c2,c3,c4q,dcf")
     ap.add_argument("--reps", type=int, default=8)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
