@@ -155,6 +155,21 @@ def _bind_tier2(L):
     _sig(L, "dpf_amd_pir_server_create_helper", I32, P, SZ, P, P, P, PP)
     _sig(L, "dpf_amd_pir_server_handle_request", I32, P, P, SZ, BUF,
          ctypes.POINTER(SZ))
+    _sig(L, "dpf_amd_pir_server_public_params", I32, P, BUF, ctypes.POINTER(SZ))
+    _sig(L, "dpf_amd_sha256_hash", I32, P, SZ, P, SZ, I32, ctypes.POINTER(I32))
+    _sig(L, "dpf_amd_hash_family_evaluate", I32, P, SZ, I32, P, SZ, I32, ctypes.POINTER(I32))
+    _sig(L, "dpf_amd_cuckoo_generate_params", I32, P, SZ, BUF, ctypes.POINTER(SZ))
+    _sig(L, "dpf_amd_cuckoo_db_create", I32, P, SZ, PP)
+    _sig(L, "dpf_amd_cuckoo_db_insert", I32, P, P, SZ, P, SZ)
+    _sig(L, "dpf_amd_cuckoo_db_place", I32, P, ctypes.POINTER(I64), I64)
+    _sig(L, "dpf_amd_cuckoo_db_place_keys", I32, P, P, SZ)
+    _sig(L, "dpf_amd_cuckoo_db_build", I32, P)
+    _sig(L, "dpf_amd_cuckoo_db_destroy", None, P)
+    _sig(L, "dpf_amd_cuckoo_db_size", I64, P)
+    _sig(L, "dpf_amd_cuckoo_db_num_selection_bits", I64, P)
+    _sig(L, "dpf_amd_cuckoo_server_create_plain", I32, P, SZ, P, PP)
+    _sig(L, "dpf_amd_cuckoo_server_create_leader", I32, P, SZ, P, P, P, PP)
+    _sig(L, "dpf_amd_cuckoo_server_create_helper", I32, P, SZ, P, P, P, PP)
 
 
 def check(code: int):

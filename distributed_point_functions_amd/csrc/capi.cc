@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "dpf_amd.h"
+#include "dpf_amd/cuckoo_hashing_sparse_dpf_pir_server.h"
 #include "dpf_amd/dense_dpf_pir_server.h"
 #include "dpf_amd/distributed_comparison_function.h"
 #include "dpf_amd/distributed_point_function.h"
@@ -34,7 +35,12 @@ struct dpf_amd_pir_db {
   }
 };
 struct dpf_amd_pir_server {
-  std::unique_ptr<DenseDpfPirServer> server;
+  std::unique_ptr<DpfPirServer> server;
+};
+struct dpf_amd_cuckoo_db {
+  std::unique_ptr<CuckooHashedDpfPirDatabase::Builder> builder =
+      std::make_unique<CuckooHashedDpfPirDatabase::Builder>();
+  std::unique_ptr<CuckooHashedDpfPirDatabase::Interface> built;
 };
 
 namespace distributed_point_functions {
@@ -407,7 +413,8 @@ int PrepareServer(const uint8_t* config, size_t config_len, dpf_amd_pir_db* db, 
   return DPF_AMD_OK;
 }
 
-int Finish(StatusOr<std::unique_ptr<DenseDpfPirServer>> s, dpf_amd_pir_server** out) {
+template <typename Server>
+int Finish(StatusOr<std::unique_ptr<Server>> s, dpf_amd_pir_server** out) {
   if (!s.ok()) return Fail(s.status());
   *out = new dpf_amd_pir_server{std::move(*s)};
   return DPF_AMD_OK;
@@ -416,6 +423,44 @@ int Finish(StatusOr<std::unique_ptr<DenseDpfPirServer>> s, dpf_amd_pir_server** 
 Status CallbackStatus(int rc, const char* what) {
   return Status(static_cast<StatusCode>(rc == DPF_AMD_OK ? DPF_AMD_INTERNAL : rc),
                 std::string(what) + " callback failed with status " + std::to_string(rc));
+}
+
+DpfPirServer::ForwardHelperRequestFn MakeSender(dpf_amd_pir_forward_fn forward, void* user) {
+  DpfPirServer::ForwardHelperRequestFn sender;
+  if (forward) {
+    sender = [forward, user](const PirRequest& helper_request,
+                             std::function<void()> while_waiting) -> StatusOr<PirResponse> {
+      const std::string req = helper_request.SerializeAsString();
+      dpf_amd_pir_call call;
+      call.while_waiting = &while_waiting;
+      int frc = forward(reinterpret_cast<const uint8_t*>(req.data()), req.size(), &call, user);
+      if (frc != DPF_AMD_OK) return CallbackStatus(frc, "ForwardHelperRequestFn");
+      if (!call.has_response)
+        return Status(StatusCode::kInternal, "ForwardHelperRequestFn returned no response");
+      PirResponse resp;
+      if (!resp.ParseFromArray(call.response.data(), call.response.size()))
+        return Status(StatusCode::kInternal, "malformed PirResponse from the Helper");
+      return resp;
+    };
+  }
+  return sender;
+}
+
+DpfPirServer::DecryptHelperRequestFn MakeDecrypter(dpf_amd_pir_decrypt_fn decrypt, void* user) {
+  DpfPirServer::DecryptHelperRequestFn decrypter;
+  if (decrypt) {
+    decrypter = [decrypt, user](const std::string& ciphertext,
+                                const std::string& info) -> StatusOr<std::string> {
+      dpf_amd_pir_call call;
+      int drc = decrypt(reinterpret_cast<const uint8_t*>(ciphertext.data()), ciphertext.size(),
+                        reinterpret_cast<const uint8_t*>(info.data()), info.size(), &call, user);
+      if (drc != DPF_AMD_OK) return CallbackStatus(drc, "DecryptHelperRequestFn");
+      if (!call.has_response)
+        return Status(StatusCode::kInternal, "DecryptHelperRequestFn returned no plaintext");
+      return call.response;
+    };
+  }
+  return decrypter;
 }
 
 }  // namespace
@@ -454,23 +499,7 @@ int dpf_amd_pir_server_create_leader(const uint8_t* config, size_t config_len, d
   std::unique_ptr<DenseDpfPirServer::Database> d;
   int rc = PrepareServer(config, config_len, db, &c, &d);
   if (rc != DPF_AMD_OK) return rc;
-  DpfPirServer::ForwardHelperRequestFn sender;
-  if (forward) {
-    sender = [forward, user](const PirRequest& helper_request,
-                             std::function<void()> while_waiting) -> StatusOr<PirResponse> {
-      const std::string req = helper_request.SerializeAsString();
-      dpf_amd_pir_call call;
-      call.while_waiting = &while_waiting;
-      int frc = forward(reinterpret_cast<const uint8_t*>(req.data()), req.size(), &call, user);
-      if (frc != DPF_AMD_OK) return CallbackStatus(frc, "ForwardHelperRequestFn");
-      if (!call.has_response)
-        return Status(StatusCode::kInternal, "ForwardHelperRequestFn returned no response");
-      PirResponse resp;
-      if (!resp.ParseFromArray(call.response.data(), call.response.size()))
-        return Status(StatusCode::kInternal, "malformed PirResponse from the Helper");
-      return resp;
-    };
-  }
+  DpfPirServer::ForwardHelperRequestFn sender = MakeSender(forward, user);
   return Finish(DenseDpfPirServer::CreateLeader(c, std::move(d), std::move(sender)), out);
 }
 
@@ -481,19 +510,7 @@ int dpf_amd_pir_server_create_helper(const uint8_t* config, size_t config_len, d
   std::unique_ptr<DenseDpfPirServer::Database> d;
   int rc = PrepareServer(config, config_len, db, &c, &d);
   if (rc != DPF_AMD_OK) return rc;
-  DpfPirServer::DecryptHelperRequestFn decrypter;
-  if (decrypt) {
-    decrypter = [decrypt, user](const std::string& ciphertext,
-                                const std::string& info) -> StatusOr<std::string> {
-      dpf_amd_pir_call call;
-      int drc = decrypt(reinterpret_cast<const uint8_t*>(ciphertext.data()), ciphertext.size(),
-                        reinterpret_cast<const uint8_t*>(info.data()), info.size(), &call, user);
-      if (drc != DPF_AMD_OK) return CallbackStatus(drc, "DecryptHelperRequestFn");
-      if (!call.has_response)
-        return Status(StatusCode::kInternal, "DecryptHelperRequestFn returned no plaintext");
-      return call.response;
-    };
-  }
+  DpfPirServer::DecryptHelperRequestFn decrypter = MakeDecrypter(decrypt, user);
   return Finish(DenseDpfPirServer::CreateHelper(c, std::move(d), std::move(decrypter)), out);
 }
 
@@ -508,6 +525,160 @@ int dpf_amd_pir_server_handle_request(const dpf_amd_pir_server* server, const ui
   StatusOr<PirResponse> resp = server->server->HandleRequest(r);
   if (!resp.ok()) return Fail(resp.status());
   return ToBuffer(resp->SerializeAsString(), response, response_len);
+}
+
+
+/* ---- Cuckoo-hashed sparse PIR ---- */
+
+int dpf_amd_sha256_hash(const uint8_t* seed, size_t seed_len, const uint8_t* input,
+                        size_t input_len, int upper_bound, int* out) {
+  if (upper_bound <= 0) return Fail(DPF_AMD_INVALID_ARGUMENT, "`upper_bound` must be positive");
+  SHA256HashFunction h(std::string(reinterpret_cast<const char*>(seed), seed_len));
+  *out = h(std::string(reinterpret_cast<const char*>(input), input_len), upper_bound);
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_hash_family_evaluate(const uint8_t* hash_family_config, size_t config_len,
+                                 int num_hash_functions, const uint8_t* input, size_t input_len,
+                                 int upper_bound, int* out) {
+  HashFamilyConfig c;
+  if (!c.ParseFromArray(hash_family_config, config_len))
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed HashFamilyConfig proto");
+  if (upper_bound <= 0) return Fail(DPF_AMD_INVALID_ARGUMENT, "`upper_bound` must be positive");
+  StatusOr<HashFamily> family = CreateHashFamilyFromConfig(c);
+  if (!family.ok()) return Fail(family.status());
+  StatusOr<std::vector<HashFunction>> fns = CreateHashFunctions(*family, num_hash_functions);
+  if (!fns.ok()) return Fail(fns.status());
+  const std::string in(reinterpret_cast<const char*>(input), input_len);
+  for (int i = 0; i < num_hash_functions; ++i) out[i] = (*fns)[i](in, upper_bound);
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_cuckoo_generate_params(const uint8_t* config, size_t config_len, uint8_t** params,
+                                   size_t* params_len) {
+  PirConfig c;
+  if (!c.ParseFromArray(config, config_len))
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed PirConfig proto");
+  StatusOr<CuckooHashingParams> p = CuckooHashingSparseDpfPirServer::GenerateParams(c);
+  if (!p.ok()) return Fail(p.status());
+  return ToBuffer(p->SerializeAsString(), params, params_len);
+}
+
+int dpf_amd_cuckoo_db_create(const uint8_t* params, size_t params_len, dpf_amd_cuckoo_db** out) {
+  CuckooHashingParams p;
+  if (!p.ParseFromArray(params, params_len))
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed CuckooHashingParams proto");
+  *out = new dpf_amd_cuckoo_db();
+  (*out)->builder->SetParams(std::move(p));
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_cuckoo_db_insert(dpf_amd_cuckoo_db* db, const uint8_t* key, size_t key_len,
+                             const uint8_t* value, size_t value_len) {
+  if (db->built) return Fail(DPF_AMD_FAILED_PRECONDITION, "Database already built");
+  db->builder->Insert({std::string(reinterpret_cast<const char*>(key), key_len),
+                       std::string(reinterpret_cast<const char*>(value), value_len)});
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_cuckoo_db_place(const dpf_amd_cuckoo_db* db, int64_t* bucket_key_lengths,
+                            int64_t num_buckets) {
+  StatusOr<std::vector<std::optional<std::string>>> t = db->builder->PlaceKeys();
+  if (!t.ok()) return Fail(t.status());
+  if (static_cast<int64_t>(t->size()) != num_buckets)
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "`num_buckets` does not match the params");
+  for (int64_t i = 0; i < num_buckets; ++i)
+    bucket_key_lengths[i] = (*t)[i] ? static_cast<int64_t>((*t)[i]->size()) : -1;
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_cuckoo_db_place_keys(const dpf_amd_cuckoo_db* db, uint8_t* keys, size_t keys_len) {
+  StatusOr<std::vector<std::optional<std::string>>> t = db->builder->PlaceKeys();
+  if (!t.ok()) return Fail(t.status());
+  size_t off = 0;
+  for (const auto& b : *t) {
+    if (!b) continue;
+    if (off + b->size() > keys_len) return Fail(DPF_AMD_INVALID_ARGUMENT, "`keys` too small");
+    memcpy(keys + off, b->data(), b->size());
+    off += b->size();
+  }
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_cuckoo_db_build(dpf_amd_cuckoo_db* db) {
+  StatusOr<std::unique_ptr<CuckooHashedDpfPirDatabase::Interface>> b = db->builder->Build();
+  if (!b.ok()) return Fail(b.status());
+  db->built = std::move(*b);
+  return DPF_AMD_OK;
+}
+
+void dpf_amd_cuckoo_db_destroy(dpf_amd_cuckoo_db* db) { delete db; }
+
+int64_t dpf_amd_cuckoo_db_size(const dpf_amd_cuckoo_db* db) {
+  return db->built ? static_cast<int64_t>(db->built->size()) : -1;
+}
+
+int64_t dpf_amd_cuckoo_db_num_selection_bits(const dpf_amd_cuckoo_db* db) {
+  return db->built ? static_cast<int64_t>(db->built->num_selection_bits()) : -1;
+}
+
+namespace {
+int PrepareCuckoo(const uint8_t* params, size_t params_len, dpf_amd_cuckoo_db* db,
+                  CuckooHashingParams* p,
+                  std::unique_ptr<CuckooHashingSparseDpfPirServer::Database>* d) {
+  if (!p->ParseFromArray(params, params_len)) {
+    delete db;
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed CuckooHashingParams proto");
+  }
+  if (db && !db->built) {
+    int rc = dpf_amd_cuckoo_db_build(db);
+    if (rc != DPF_AMD_OK) {
+      delete db;
+      return rc;
+    }
+  }
+  if (db) *d = std::move(db->built);
+  delete db;
+  return DPF_AMD_OK;
+}
+}  // namespace
+
+int dpf_amd_cuckoo_server_create_plain(const uint8_t* params, size_t params_len,
+                                       dpf_amd_cuckoo_db* db, dpf_amd_pir_server** out) {
+  CuckooHashingParams p;
+  std::unique_ptr<CuckooHashingSparseDpfPirServer::Database> d;
+  int rc = PrepareCuckoo(params, params_len, db, &p, &d);
+  if (rc != DPF_AMD_OK) return rc;
+  return Finish(CuckooHashingSparseDpfPirServer::CreatePlain(std::move(p), std::move(d)), out);
+}
+
+int dpf_amd_cuckoo_server_create_leader(const uint8_t* params, size_t params_len,
+                                        dpf_amd_cuckoo_db* db, dpf_amd_pir_forward_fn forward,
+                                        void* user, dpf_amd_pir_server** out) {
+  CuckooHashingParams p;
+  std::unique_ptr<CuckooHashingSparseDpfPirServer::Database> d;
+  int rc = PrepareCuckoo(params, params_len, db, &p, &d);
+  if (rc != DPF_AMD_OK) return rc;
+  return Finish(CuckooHashingSparseDpfPirServer::CreateLeader(std::move(p), std::move(d),
+                                                             MakeSender(forward, user)),
+                out);
+}
+
+int dpf_amd_cuckoo_server_create_helper(const uint8_t* params, size_t params_len,
+                                        dpf_amd_cuckoo_db* db, dpf_amd_pir_decrypt_fn decrypt,
+                                        void* user, dpf_amd_pir_server** out) {
+  CuckooHashingParams p;
+  std::unique_ptr<CuckooHashingSparseDpfPirServer::Database> d;
+  int rc = PrepareCuckoo(params, params_len, db, &p, &d);
+  if (rc != DPF_AMD_OK) return rc;
+  return Finish(CuckooHashingSparseDpfPirServer::CreateHelper(std::move(p), std::move(d),
+                                                             MakeDecrypter(decrypt, user)),
+                out);
+}
+
+int dpf_amd_pir_server_public_params(const dpf_amd_pir_server* server, uint8_t** params,
+                                     size_t* params_len) {
+  return ToBuffer(server->server->GetPublicParams().SerializeAsString(), params, params_len);
 }
 
 }  // extern "C"

@@ -649,12 +649,95 @@ bool DcfKey::ParseFromArray(const void* data, size_t size) {
   return r.ok();
 }
 
+// --- pir/hashing/hash_family_config.proto, CuckooHashingParams ---
+std::string HashFamilyConfig::SerializeAsString() const {
+  Writer w;
+  w.U64(1, static_cast<uint64_t>(static_cast<int64_t>(hash_family_)));
+  w.Bytes(2, seed_);
+  return w.Take();
+}
+bool HashFamilyConfig::ParseFromArray(const void* data, size_t size) {
+  *this = HashFamilyConfig();
+  Reader r(data, size);
+  DPF_FOR_EACH_FIELD(r, f, wt) {
+    uint64_t v;
+    const uint8_t* d;
+    size_t l;
+    if (f == 1 && wt == 0) {
+      if (!r.Varint(&v)) return false;
+      hash_family_ = static_cast<int>(v);
+    } else if (f == 2 && wt == 2) {
+      if (!r.Bytes(&d, &l)) return false;
+      seed_.assign(reinterpret_cast<const char*>(d), l);
+    } else if (!r.Skip(wt)) {
+      return false;
+    }
+  }
+  return r.ok();
+}
+
+std::string CuckooHashingParams::SerializeAsString() const {
+  Writer w;
+  if (has_hash_family_config_) w.Message(1, hash_family_config_.SerializeAsString());
+  w.U64(2, static_cast<uint64_t>(static_cast<int64_t>(num_hash_functions_)));
+  w.U64(3, static_cast<uint64_t>(num_buckets_));
+  return w.Take();
+}
+bool CuckooHashingParams::ParseFromArray(const void* data, size_t size) {
+  *this = CuckooHashingParams();
+  Reader r(data, size);
+  DPF_FOR_EACH_FIELD(r, f, wt) {
+    uint64_t v;
+    const uint8_t* d;
+    size_t l;
+    if (f == 1 && wt == 2) {
+      if (!r.Bytes(&d, &l) || !mutable_hash_family_config()->ParseFromArray(d, l)) return false;
+    } else if (f == 2 && wt == 0) {
+      if (!r.Varint(&v)) return false;
+      num_hash_functions_ = static_cast<int32_t>(v);
+    } else if (f == 3 && wt == 0) {
+      if (!r.Varint(&v)) return false;
+      num_buckets_ = static_cast<int64_t>(v);
+    } else if (!r.Skip(wt)) {
+      return false;
+    }
+  }
+  return r.ok();
+}
+
+std::string PirServerPublicParams::SerializeAsString() const {
+  Writer w;
+  if (case_ == kCuckooHashingSparseDpfPirServerParams) w.Message(1, cuckoo_.SerializeAsString());
+  return w.Take();
+}
+bool PirServerPublicParams::ParseFromArray(const void* data, size_t size) {
+  *this = PirServerPublicParams();
+  Reader r(data, size);
+  DPF_FOR_EACH_FIELD(r, f, wt) {
+    const uint8_t* d;
+    size_t l;
+    if (f == 1 && wt == 2) {
+      if (!r.Bytes(&d, &l) ||
+          !mutable_cuckoo_hashing_sparse_dpf_pir_server_params()->ParseFromArray(d, l))
+        return false;
+    } else if (!r.Skip(wt)) {
+      return false;
+    }
+  }
+  return r.ok();
+}
+
 std::string PirConfig::SerializeAsString() const {
   Writer w;
   if (case_ == kDenseDpfPirConfig) {
     Writer d;
     d.U64(1, static_cast<uint64_t>(dense_.num_elements()));
     w.Message(1, d.Take());
+  } else if (case_ == kCuckooHashingSparseDpfPirConfig) {
+    Writer d;
+    d.U64(1, static_cast<uint64_t>(static_cast<int64_t>(cuckoo_.hash_family())));
+    d.U64(2, static_cast<uint64_t>(cuckoo_.num_elements()));
+    w.Message(2, d.Take());
   }
   return w.Take();
 }
@@ -664,15 +747,18 @@ bool PirConfig::ParseFromArray(const void* data, size_t size) {
   DPF_FOR_EACH_FIELD(r, f, wt) {
     const uint8_t* d;
     size_t l;
-    if (f == 1 && wt == 2) {
+    if ((f == 1 || f == 2) && wt == 2) {
       if (!r.Bytes(&d, &l)) return false;
-      DenseDpfPirConfig* c = mutable_dense_dpf_pir_config();
       Reader cr(d, l);
+      if (f == 1) mutable_dense_dpf_pir_config();
+      else mutable_cuckoo_hashing_sparse_dpf_pir_config();
       DPF_FOR_EACH_FIELD(cr, cf, cwt) {
         uint64_t v;
-        if (cf == 1 && cwt == 0) {
+        if (cwt == 0 && (cf == 1 || (f == 2 && cf == 2))) {
           if (!cr.Varint(&v)) return false;
-          c->set_num_elements(static_cast<int64_t>(v));
+          if (f == 1) dense_.set_num_elements(static_cast<int64_t>(v));
+          else if (cf == 1) cuckoo_.set_hash_family(static_cast<int>(v));
+          else cuckoo_.set_num_elements(static_cast<int64_t>(v));
         } else if (!cr.Skip(cwt)) {
           return false;
         }

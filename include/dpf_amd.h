@@ -395,6 +395,70 @@ int dpf_amd_pir_server_handle_request(const dpf_amd_pir_server* server,
                                       size_t request_len, uint8_t** response,
                                       size_t* response_len);
 
+/* ---- Cuckoo-hashed sparse (keyword) PIR ------------------------------------
+ * The reference's CuckooHashingSparseDpfPirServer
+ * (pir/cuckoo_hashing_sparse_dpf_pir_server.h:37-125) over a
+ * CuckooHashedDpfPirDatabase (pir/cuckoo_hashed_dpf_pir_database.h:37-110):
+ * keys are cuckoo-placed into num_buckets buckets on the host, the key and
+ * value tables live in HBM, and one request is one DPF expansion per key plus
+ * two HBM scans. Servers share the dpf_amd_pir_server handle (HandleRequest,
+ * destroy) with the dense server. */
+typedef struct dpf_amd_cuckoo_db dpf_amd_cuckoo_db;
+
+/* SHA256HashFunction(seed)(input, upper_bound)
+ * (pir/hashing/sha256_hash_family.cc:59-86). */
+int dpf_amd_sha256_hash(const uint8_t* seed, size_t seed_len,
+                        const uint8_t* input, size_t input_len, int upper_bound,
+                        int* out);
+/* CreateHashFunctions(CreateHashFamilyFromConfig(config), n)[i](input, ub)
+ * for i < n into out[0..n) (pir/hashing/hash_family.cc:27-39,
+ * hash_family_config.cc:27-45); `hash_family_config` is a serialized
+ * HashFamilyConfig. */
+int dpf_amd_hash_family_evaluate(const uint8_t* hash_family_config,
+                                 size_t config_len, int num_hash_functions,
+                                 const uint8_t* input, size_t input_len,
+                                 int upper_bound, int* out);
+/* CuckooHashingSparseDpfPirServer::GenerateParams (.cc:46-65): serialized
+ * PirConfig in, serialized CuckooHashingParams out (free with dpf_amd_free). */
+int dpf_amd_cuckoo_generate_params(const uint8_t* config, size_t config_len,
+                                   uint8_t** params, size_t* params_len);
+/* CuckooHashedDpfPirDatabase::Builder (SetParams / Insert / Build). */
+int dpf_amd_cuckoo_db_create(const uint8_t* params, size_t params_len,
+                             dpf_amd_cuckoo_db** out);
+int dpf_amd_cuckoo_db_insert(dpf_amd_cuckoo_db* db, const uint8_t* key,
+                             size_t key_len, const uint8_t* value,
+                             size_t value_len);
+/* Host-only cuckoo placement of the inserted keys (the first half of
+ * Build(), cuckoo_hashed_dpf_pir_database.cc:100-131): bucket_key_lengths[b]
+ * = length of the key in bucket b, or -1 when empty; place_keys writes the
+ * placed keys back to back in bucket order. */
+int dpf_amd_cuckoo_db_place(const dpf_amd_cuckoo_db* db,
+                            int64_t* bucket_key_lengths, int64_t num_buckets);
+int dpf_amd_cuckoo_db_place_keys(const dpf_amd_cuckoo_db* db, uint8_t* keys,
+                                 size_t keys_len);
+int dpf_amd_cuckoo_db_build(dpf_amd_cuckoo_db* db);
+void dpf_amd_cuckoo_db_destroy(dpf_amd_cuckoo_db* db);
+int64_t dpf_amd_cuckoo_db_size(const dpf_amd_cuckoo_db* db);
+int64_t dpf_amd_cuckoo_db_num_selection_bits(const dpf_amd_cuckoo_db* db);
+/* CuckooHashingSparseDpfPirServer::{CreatePlain, CreateLeader, CreateHelper}
+ * (.cc:67-128) from serialized CuckooHashingParams; take ownership of `db`
+ * (built here if needed). */
+int dpf_amd_cuckoo_server_create_plain(const uint8_t* params, size_t params_len,
+                                       dpf_amd_cuckoo_db* db,
+                                       dpf_amd_pir_server** out);
+int dpf_amd_cuckoo_server_create_leader(const uint8_t* params,
+                                        size_t params_len, dpf_amd_cuckoo_db* db,
+                                        dpf_amd_pir_forward_fn forward,
+                                        void* user, dpf_amd_pir_server** out);
+int dpf_amd_cuckoo_server_create_helper(const uint8_t* params,
+                                        size_t params_len, dpf_amd_cuckoo_db* db,
+                                        dpf_amd_pir_decrypt_fn decrypt,
+                                        void* user, dpf_amd_pir_server** out);
+/* PirServer::GetPublicParams (pir/pir_server.h): serialized
+ * PirServerPublicParams. */
+int dpf_amd_pir_server_public_params(const dpf_amd_pir_server* server,
+                                     uint8_t** params, size_t* params_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -295,14 +295,68 @@ class DenseDpfPirConfig {
   int64_t num_elements_ = 0;
 };
 
+// pir/hashing/hash_family_config.proto:22-35
+class HashFamilyConfig {
+ public:
+  enum HashFamily { HASH_FAMILY_UNSPECIFIED = 0, HASH_FAMILY_SHA256 = 1 };
+  DPF_AMD_SCALAR_FIELD(int, hash_family)
+  const std::string& seed() const { return seed_; }
+  std::string* mutable_seed() { return &seed_; }
+  void set_seed(std::string s) { seed_ = std::move(s); }
+  std::string SerializeAsString() const;
+  bool ParseFromArray(const void* data, size_t size);
+
+ private:
+  int hash_family_ = HASH_FAMILY_UNSPECIFIED;
+  std::string seed_;
+};
+
+// private_information_retrieval.proto: CuckooHashingSparseDpfPirConfig
+class CuckooHashingSparseDpfPirConfig {
+ public:
+  DPF_AMD_SCALAR_FIELD(int, hash_family)
+  DPF_AMD_SCALAR_FIELD(int64_t, num_elements)
+
+ private:
+  int hash_family_ = HashFamilyConfig::HASH_FAMILY_UNSPECIFIED;
+  int64_t num_elements_ = 0;
+};
+
+// private_information_retrieval.proto: CuckooHashingParams
+class CuckooHashingParams {
+ public:
+  DPF_AMD_MESSAGE_FIELD(HashFamilyConfig, hash_family_config)
+  DPF_AMD_SCALAR_FIELD(int32_t, num_hash_functions)
+  DPF_AMD_SCALAR_FIELD(int64_t, num_buckets)
+  std::string SerializeAsString() const;
+  bool ParseFromArray(const void* data, size_t size);
+
+ private:
+  bool has_hash_family_config_ = false;
+  HashFamilyConfig hash_family_config_;
+  int32_t num_hash_functions_ = 0;
+  int64_t num_buckets_ = 0;
+};
+
 class PirConfig {
  public:
-  enum WrappedPirConfigCase { WRAPPED_PIR_CONFIG_NOT_SET = 0, kDenseDpfPirConfig = 1 };
+  enum WrappedPirConfigCase {
+    WRAPPED_PIR_CONFIG_NOT_SET = 0,
+    kDenseDpfPirConfig = 1,
+    kCuckooHashingSparseDpfPirConfig = 2
+  };
   WrappedPirConfigCase wrapped_pir_config_case() const { return case_; }
   const DenseDpfPirConfig& dense_dpf_pir_config() const { return dense_; }
   DenseDpfPirConfig* mutable_dense_dpf_pir_config() {
     case_ = kDenseDpfPirConfig;
     return &dense_;
+  }
+  const CuckooHashingSparseDpfPirConfig& cuckoo_hashing_sparse_dpf_pir_config() const {
+    return cuckoo_;
+  }
+  CuckooHashingSparseDpfPirConfig* mutable_cuckoo_hashing_sparse_dpf_pir_config() {
+    case_ = kCuckooHashingSparseDpfPirConfig;
+    return &cuckoo_;
   }
   std::string SerializeAsString() const;
   bool ParseFromArray(const void* data, size_t size);
@@ -310,6 +364,7 @@ class PirConfig {
  private:
   WrappedPirConfigCase case_ = WRAPPED_PIR_CONFIG_NOT_SET;
   DenseDpfPirConfig dense_;
+  CuckooHashingSparseDpfPirConfig cuckoo_;
 };
 
 class DpfPirRequest {
@@ -428,7 +483,25 @@ class PirResponse {
 
 class PirServerPublicParams {
  public:
+  enum WrappedPirServerPublicParamsCase {
+    WRAPPED_PIR_SERVER_PUBLIC_PARAMS_NOT_SET = 0,
+    kCuckooHashingSparseDpfPirServerParams = 1
+  };
   static const PirServerPublicParams& default_instance();
+  WrappedPirServerPublicParamsCase wrapped_pir_server_public_params_case() const { return case_; }
+  const CuckooHashingParams& cuckoo_hashing_sparse_dpf_pir_server_params() const {
+    return cuckoo_;
+  }
+  CuckooHashingParams* mutable_cuckoo_hashing_sparse_dpf_pir_server_params() {
+    case_ = kCuckooHashingSparseDpfPirServerParams;
+    return &cuckoo_;
+  }
+  std::string SerializeAsString() const;
+  bool ParseFromArray(const void* data, size_t size);
+
+ private:
+  WrappedPirServerPublicParamsCase case_ = WRAPPED_PIR_SERVER_PUBLIC_PARAMS_NOT_SET;
+  CuckooHashingParams cuckoo_;
 };
 
 // Wire helpers for the remaining messages.
