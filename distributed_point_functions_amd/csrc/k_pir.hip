@@ -6,6 +6,23 @@
 
 namespace dpf_amd {
 
+// DB records are read exactly once per scan pass, so they are issued as
+// nontemporal loads (DPF_AMD_SCAN_NT=1, default): measured on MI355X at
+// 2^26 x 256 B, Q = 1 2.75 -> 2.47 ms (6.25 -> 6.94 TB/s), Q = 8 2.96 -> 2.55,
+// Q = 64 18.8 -> 15.5 ms.  DPF_AMD_SCAN_NT=0 restores plain loads for A/B.
+#ifndef DPF_AMD_SCAN_NT
+#define DPF_AMD_SCAN_NT 1
+#endif
+__device__ __forceinline__ uint4 LoadRecordWord(const uint4* p) {
+#if DPF_AMD_SCAN_NT
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return *p;
+#endif
+}
+
 // ----------------------------------------------------------------------------
 // Gather / fold helpers
 // ----------------------------------------------------------------------------
@@ -183,7 +200,7 @@ __global__ __launch_bounds__(kScanBlock) void KPirScan(ScanArgs a) {
         rr[u] = it + u * G + my_rec;
         const int64_t rec = rec0 + rr[u];
         const bool ok = active && rr[u] < 128 && rec < a.num_records;
-        v[u] = ok ? a.db[rec * a.C + my_chunk] : make_uint4(0, 0, 0, 0);
+        v[u] = ok ? LoadRecordWord(&a.db[rec * a.C + my_chunk]) : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int u = 0; u < kScanUnroll; ++u) {
@@ -241,7 +258,7 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int64_t rec = rec0 + d * 32 + k0 + u * G + my_rec;
-          v[u] = (full || rec < a.num_records) ? a.db[rec * a.C + my_chunk]
+          v[u] = (full || rec < a.num_records) ? LoadRecordWord(&a.db[rec * a.C + my_chunk])
                                                 : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
