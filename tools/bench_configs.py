@@ -14,6 +14,11 @@ c4q dense-PIR XOR scan at Q = 8 and 64 over 2^26 x 256 B (kernel only)
 dcf DistributedComparisonFunction BatchEvaluate, log_domain 32, uint64
     (distributed_comparison_function_benchmark.cc:31-63 shape): 1024 keys
     via the Tier-2 API, and 2^20 (key, point) pairs through the fused kernel
+cuckoo  cuckoo-hashed sparse PIR: 2^20 keyword records
+    (16-byte keys, 240-byte values), 1.5 x 2^20 buckets, 3 SHA-256 hash
+    functions; two plain servers, one keyword query (3 DPF keys per server)
+    through HandleRequest (wire decode, device DPF selection, key- and
+    value-table scans, response), reconstructed by the client
 
 Kernel times are HIP events on the launch stream; API times are wall clock.
 Every config also checks its outputs (share-sum / reconstruction).
@@ -348,9 +353,50 @@ def dcf(dev, reps):
             "kernel_evaluations_per_s": n / t_k, "correct": bool(ok)}
 
 
+def cuckoo(dev, reps):
+    from distributed_point_functions_amd import cuckoo_pir as C
+    from distributed_point_functions_amd import dpf as D
+    n, vlen = 1 << 20, 240
+    rng = np.random.default_rng(7)
+    keys = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    vals = rng.integers(0, 256, (n, vlen), dtype=np.uint8)
+    nb = int(1.5 * n)
+    params = C.cuckoo_hashing_params(bytes(range(16)), nb)
+    t0 = time.perf_counter()
+    servers = []
+    for _ in range(2):
+        db = C.CuckooHashedDpfPirDatabase(params)
+        for i in range(n):
+            db.insert(keys[i].tobytes(), vals[i].tobytes())
+        servers.append(C.CuckooHashingSparseDpfPirServer.create_plain(params, db))
+    t_build = (time.perf_counter() - t0) / 2
+    dpf = D.DistributedPointFunction.create(
+        D.DpfParameters(max(0, (nb - 1).bit_length()), V.XorWrapper(128)))
+    client = C.CuckooHashingSparseDpfPirClient(params, dpf)
+    qi = [int(x) for x in rng.integers(0, n, 4)]
+    queries = [keys[i].tobytes() for i in qi] + [b"not-a-stored-key"]
+    r0, r1 = client.create_requests(queries)
+    resp0 = servers[0].handle_request(r0)
+    resp1 = servers[1].handle_request(r1)
+    got = client.handle_responses(queries, resp0, resp1)
+    # a key can be left in the unserved stash (reference semantics), so only
+    # check that every served answer is the stored value
+    ok = got[-1] is None and all(g is None or g == vals[i].tobytes()
+                                 for g, i in zip(got, qi))
+    served = sum(g is not None for g in got[:-1])
+    t = wall_time(lambda: servers[0].handle_request(r0), reps)
+    table_bytes = nb * (16 + vlen)
+    return {"config": "cuckoo", "workload": "cuckoo-hashed sparse PIR, 2^20 x (16 B key, "
+            "240 B value), 1.5x buckets, 3 hash functions",
+            "queries_per_request": len(queries), "dpf_keys_per_request": 3 * len(queries),
+            "handle_request_ms": t * 1e3,
+            "table_GBps_per_key": 3 * len(queries) * table_bytes / t / 1e9,
+            "db_build_s": t_build, "served": served, "correct": bool(ok)}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="c1,c2,c3,c4q,dcf")
+    ap.add_argument("--only", default="c1,c2,c3,c4q,dcf,cuckoo")
     ap.add_argument("--reps", type=int, default=8)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
