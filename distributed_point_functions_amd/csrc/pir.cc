@@ -104,10 +104,19 @@ StatusOr<std::unique_ptr<DenseDpfPirDatabase::Interface>> DenseDpfPirDatabase::B
   // width the wave-uniform KPirScanG path handles (16, 32, 64, 128, 256,
   // 512 B or a multiple of 1 KiB; PirScanGroup) — at most 2x the bytes, for a
   // scan several times faster than the generic one (e.g. 240-byte cuckoo
-  // values). Responses are still max_value_size_ bytes.
-  db->stride_ = ScanFriendlyStride(std::max<int64_t>(16, AlignBytes(max_size)));
-  const int64_t bytes = std::max<int64_t>(16, n * db->stride_);
-  DPF_RETURN_IF_ERROR(HipStatus(hipMalloc(&db->records_, bytes), "hipMalloc(database)"));
+  // values). Responses are still max_value_size_ bytes. When the padded
+  // table does not fit in HBM, the plain 16-byte-aligned stride is used.
+  const int64_t aligned = std::max<int64_t>(16, AlignBytes(max_size));
+  db->stride_ = ScanFriendlyStride(aligned);
+  int64_t bytes = std::max<int64_t>(16, n * db->stride_);
+  if (db->stride_ != aligned && hipMalloc(&db->records_, bytes) != hipSuccess) {
+    (void)hipGetLastError();  // clear the failed allocation's sticky error
+    db->records_ = nullptr;
+    db->stride_ = aligned;
+    bytes = std::max<int64_t>(16, n * db->stride_);
+  }
+  if (db->records_ == nullptr)
+    DPF_RETURN_IF_ERROR(HipStatus(hipMalloc(&db->records_, bytes), "hipMalloc(database)"));
   DPF_RETURN_IF_ERROR(HipStatus(hipMemset(db->records_, 0, bytes), "hipMemset(database)"));
   // Upload in 64 MiB chunks of zero-padded fixed-stride rows.
   const int64_t rows_per_chunk = std::max<int64_t>(1, (64 << 20) / db->stride_);
