@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -16,6 +17,8 @@
 namespace dpf_amd {
 
 namespace {
+
+std::atomic<int> g_expand_depth{0};  // dpf_amd_set_expand_depth (tests)
 
 int GridFor(int64_t items, int block, int max_blocks) {
   int64_t g = (items + block - 1) / block;
@@ -234,6 +237,8 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
     D = num_levels;
   // For small problems prefer more threads over deep DFS.
   while (D > 2 && ((leaf_end - leaf_begin) >> D) < 65536) D = (D == 8) ? 4 : 2;
+  const int forced = g_expand_depth.load(std::memory_order_relaxed);
+  if (forced > 0 && forced <= num_levels) D = forced;
   ExpandArgs a;
   a.root_seeds = (const uint4*)root_seeds;
   a.root_cb = root_control_bits;
@@ -250,6 +255,11 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
   // LaunchExpand caps the grid (DPF_EXPAND_MAX_GRID).
   const int grid = GridFor(a.chunk_end - a.chunk_begin, kExpandBlock, INT32_MAX);
   return LaunchExpandForType(D, grid, (hipStream_t)stream, a, dev);
+}
+
+int dpf_amd_set_expand_depth(int depth) {
+  if (depth != 0 && depth != 1 && depth != 2 && depth != 4 && depth != 8) return -1;
+  return g_expand_depth.exchange(depth);
 }
 
 // Shared body of dpf_amd_evaluate_points{,_batched}.

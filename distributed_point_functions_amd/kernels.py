@@ -97,6 +97,25 @@ def expand_and_correct(root_seeds, root_control_bits, num_levels, cw_seeds, ccl,
     return out
 
 
+class forced_expand_depth:
+    """Context manager forcing the fused expansion kernel's register-DFS
+    depth (dpf_amd_set_expand_depth; tests run the deep kernels that large
+    launches select on small domains)."""
+
+    def __init__(self, depth: int):
+        self.depth = depth
+
+    def __enter__(self):
+        prev = _lib.lib().dpf_amd_set_expand_depth(self.depth)
+        if prev < 0:
+            raise ValueError("expand depth must be 0, 1, 2, 4 or 8")
+        self.prev = prev
+        return self
+
+    def __exit__(self, *exc):
+        _lib.lib().dpf_amd_set_expand_depth(self.prev)
+
+
 def evaluate_points(seeds, control_bits, paths, paths_rightshift, num_levels,
                     cw_seeds, ccl, ccr, desc, block_index=None, party=None,
                     party_all: int = 0, value_corrections=None,

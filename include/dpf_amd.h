@@ -129,6 +129,13 @@ int dpf_amd_expand_and_correct(
     int corrected_elements_per_block, int64_t leaf_begin, int64_t leaf_end,
     void* out, void* stream);
 
+/* Testing knob (process-wide): forces the register-DFS depth D of the fused
+ * expansion kernel to 1, 2, 4 or 8 whenever num_levels >= D, so the deep
+ * kernels that large launches select can be checked on small domains.
+ * 0 restores the automatic choice.  Returns the previous setting, or -1 for
+ * an invalid depth (setting unchanged). */
+int dpf_amd_set_expand_depth(int depth);
+
 /* Fused single-path evaluation: EvaluateSeeds from the given seeds along
  * `paths` (one AES per level, per-lane key select) + HashExpandedSeeds +
  * correction of element block_index[i] (EvaluateAtImpl h:1013-1063 and the

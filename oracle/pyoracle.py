@@ -478,6 +478,19 @@ class Dpf:
         _check(lib().or_evaluate_at(self._h, key._p, level, _ptr(pw), len(points), _ptr(out)))
         return self._elements(out, ns, len(points))
 
+    def evaluate_at_words(self, key: Key, level: int, points) -> np.ndarray:
+        """As evaluate_at but returns the raw (n, ns, 2) uint64 words;
+        `points` may be an (n, 2) uint64 {lo, hi} array."""
+        ns = num_scalars(self.levels[level][1])
+        if isinstance(points, np.ndarray):
+            pw = np.ascontiguousarray(points, dtype=np.uint64).reshape(-1)
+        else:
+            pw = u128_words(points) if len(points) else np.zeros(2, np.uint64)
+        n = len(pw) // 2
+        out = np.zeros(max(2 * ns * n, 2), dtype=np.uint64)
+        _check(lib().or_evaluate_at(self._h, key._p, level, _ptr(pw), n, _ptr(out)))
+        return out[:2 * ns * n].reshape(n, ns, 2)
+
     def expand_subtree_words(self, key: Key, first_block: int, log_blocks: int,
                              out: np.ndarray = None) -> np.ndarray:
         h = len(self.levels) - 1

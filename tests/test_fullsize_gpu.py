@@ -1,0 +1,254 @@
+"""Parity of the expansion kernels that the production launches select, and
+of the benchmarked configuration at its full size.
+
+`dpf_amd_expand_and_correct` picks the register-DFS depth D of KExpand<D>
+from the launch size (kernels_capi.cc): D = 8 once a launch covers >= 2^24
+tree leaves, D = 4 from 2^20.  These tests
+  * force D in {1, 2, 4, 8} (dpf_amd_set_expand_depth) on small domains and
+    compare every output of every value type with the oracle;
+  * run the automatic choice at sizes where it picks D = 4 (2^20 tree
+    leaves) and D = 8 (2^24) and compare every output with the oracle;
+  * run the c5 bench configuration itself (log_domain_size 32,
+    Tuple<uint32, IntModN<uint64, 2^64-59>>, the KExpand<8, EmitU32ModN64>
+    launch the bench times) for both parties: the share sum over all 2^32
+    leaves is checked on the device (beta at alpha, 0 elsewhere — the
+    reference's own full-domain property, distributed_point_function_test.cc:
+    652-696), sampled 2^20-leaf subtrees are compared bit-exactly with the
+    oracle, leaf-range slices above 2^31 equal the matching part of the full
+    launch, and bench.py's 8-rank subtree split (sharding.block_range), run
+    rank by rank on this GPU, reproduces the 1-rank output.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as po
+
+from tests.test_kernels_gpu import P64, TYPES, _keys, u8
+
+pytestmark = pytest.mark.gpu
+
+C5 = ("tuple", [("int", 32), ("intmodn", 64, P64)])
+
+
+@pytest.fixture(scope="module")
+def K(cuda):
+    from distributed_point_functions_amd import kernels
+    return kernels
+
+
+def _key_arrays(K, cuda, d, key):
+    L = d.hierarchy_to_tree(0)
+    return dict(
+        seed=K.u128_tensor([key.seed], cuda), cb=u8([key.party], cuda), L=L,
+        cw=K.u128_tensor(key.cw_seeds()[:L] or [0], cuda), ccl=u8(key.ccl()[:L] or [0], cuda),
+        ccr=u8(key.ccr()[:L] or [0], cuda), corr=key.value_corrections()[0], party=key.party)
+
+
+def _expand(K, cuda, d, key, spec, leaf_begin=0, leaf_end=None, out=None):
+    """Device expansion (uint8 tensor of host-layout T) through the C ABI."""
+    from distributed_point_functions_amd import value_types as vtm
+    vt = vtm.from_spec(spec)
+    ka = _key_arrays(K, cuda, d, key)
+    cepb = 1 << (d.levels[0][0] - ka["L"])
+    return K.expand_and_correct(ka["seed"], ka["cb"], ka["L"], ka["cw"], ka["ccl"], ka["ccr"],
+                                vt.descriptor(d.blocks_needed(0)), ka["corr"], ka["party"],
+                                cepb, leaf_begin, leaf_end, out)
+
+
+def _chunked_equal(a, b, chunk=1 << 32) -> bool:
+    """torch.equal without a full-size temporary (64 GiB buffers)."""
+    import torch
+    if a.numel() != b.numel():
+        return False
+    return all(torch.equal(a[i:i + chunk], b[i:i + chunk]) for i in range(0, a.numel(), chunk))
+
+
+def _assert_host_layout_equals_words(spec, got: np.ndarray, words: np.ndarray, what=""):
+    """got: host-layout bytes of n elements; words: oracle (n, ns, 2) uint64."""
+    from distributed_point_functions_amd import value_types as vtm
+    vt = vtm.from_spec(spec)
+    arr = got.view(vt.numpy_dtype())
+    assert arr.shape[0] == words.shape[0], what
+    for i, s in enumerate(vt.scalars()):
+        col = arr["f%d" % i]
+        if s.bits == 128:
+            ok = np.array_equal(col[:, 0], words[:, i, 0]) and \
+                np.array_equal(col[:, 1], words[:, i, 1])
+        else:
+            ok = np.array_equal(col.astype(np.uint64), words[:, i, 0]) and \
+                not words[:, i, 1].any()
+        if not ok:
+            bad = np.nonzero(col.astype(np.uint64) != words[:, i, 0])[0] \
+                if s.bits != 128 else np.nonzero(col[:, 0] != words[:, i, 0])[0]
+            pytest.fail("%s: scalar %d differs from the oracle at %d elements (first %s)" %
+                        (what, i, len(bad), bad[:5]))
+
+
+# ---------------------------------------------------------------------------
+# Every DFS depth, every value type, whole domain vs oracle
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("depth", [1, 2, 4, 8])
+@pytest.mark.parametrize("spec", TYPES, ids=[repr(t) for t in TYPES])
+def test_forced_depth_matches_oracle(K, cuda, spec, depth):
+    d, k0, k1, alpha, beta = _keys(spec, 14, seed=depth)
+    assert d.hierarchy_to_tree(0) >= depth
+    with K.forced_expand_depth(depth):
+        for key in (k0, k1):
+            want = d.evaluate_until_words(0, [], d.create_evaluation_context(key))
+            got = _expand(K, cuda, d, key, spec).cpu().numpy()
+            _assert_host_layout_equals_words(spec, got, want, "party %d" % key.party)
+
+
+@pytest.mark.parametrize("depth", [4, 8])
+def test_forced_depth_leaf_ranges(K, cuda, depth):
+    """Ragged leaf ranges that start and end inside a 2^D-leaf subtree."""
+    d, k0, _, _, _ = _keys(C5, 15, seed=3)
+    want = d.evaluate_until_words(0, [], d.create_evaluation_context(k0))
+    n = 1 << d.hierarchy_to_tree(0)
+    with K.forced_expand_depth(depth):
+        for lo, hi in [(0, n), (1, n - 1), (255, 257), (3000, 3001), (4097, 20000),
+                       (n - 300, n)]:
+            got = _expand(K, cuda, d, k0, C5, lo, hi).cpu().numpy()
+            _assert_host_layout_equals_words(C5, got, want[lo:hi], "[%d, %d)" % (lo, hi))
+
+
+def test_forced_depth_knob_validates():
+    from distributed_point_functions_amd import kernels as K
+    with pytest.raises(ValueError):
+        with K.forced_expand_depth(3):
+            pass
+
+
+# ---------------------------------------------------------------------------
+# The automatic choice at the sizes where it selects D = 4 and D = 8
+# ---------------------------------------------------------------------------
+
+AUTO = [  # (spec, log_domain) -> tree levels L; D = 4 at L = 20, D = 8 at L = 24
+    (C5, 20), (C5, 24),
+    (("int", 64), 21), (("int", 64), 25),
+    (("xor", 128), 20), (("xor", 128), 24),
+]
+
+
+@pytest.mark.parametrize("spec,ld", AUTO, ids=["%r-ld%d" % a for a in AUTO])
+def test_production_depth_full_domain_matches_oracle(K, cuda, spec, ld):
+    import torch
+    d, k0, k1, alpha, beta = _keys(spec, ld, seed=11)
+    L = d.hierarchy_to_tree(0)
+    assert L in (20, 24)
+    for key in (k0, k1):
+        want = d.evaluate_until_words(0, [], d.create_evaluation_context(key))
+        got = _expand(K, cuda, d, key, spec).cpu().numpy()
+        _assert_host_layout_equals_words(spec, got, want, "ld %d party %d" % (ld, key.party))
+        del got, want
+    torch.cuda.empty_cache()
+
+
+# ---------------------------------------------------------------------------
+# c5 at full size: log_domain_size 32, both parties, 2 x 64 GiB in HBM
+# ---------------------------------------------------------------------------
+
+@pytest.fixture(scope="module")
+def c5_full(K, cuda):
+    import torch
+    d, k0, k1, alpha, beta = _keys(C5, 32, seed=5)
+    assert d.hierarchy_to_tree(0) == 32
+    n = 1 << 32
+    outs = []
+    for key in (k0, k1):
+        out = torch.empty(n * 16, dtype=torch.uint8, device=cuda)
+        _expand(K, cuda, d, key, C5, out=out)
+        outs.append(out)
+    torch.cuda.synchronize()
+    yield dict(d=d, keys=(k0, k1), alpha=alpha, beta=beta, outs=outs, n=n)
+    outs.clear()
+    torch.cuda.empty_cache()
+
+
+def test_c5_full_domain_share_sum_on_device(c5_full):
+    """out0 + out1 == beta at alpha and 0 at every other of the 2^32 leaves
+    (u32 wraps mod 2^32, IntModN adds mod p = 2^64 - 59)."""
+    import torch
+    n, alpha = c5_full["n"], c5_full["alpha"]
+    a = c5_full["outs"][0].view(torch.int64).view(-1, 2)
+    b = c5_full["outs"][1].view(torch.int64).view(-1, 2)
+    chunk = 1 << 27
+    nonzero = []
+    for c0 in range(0, n, chunk):
+        x, y = a[c0:c0 + chunk], b[c0:c0 + chunk]
+        # IntModN share in word 0 (< p < 2^64): a + b in {0, p}; p = -59 as int64
+        s1 = x[:, 0] + y[:, 0]
+        zero1 = (s1 == -59) | ((x[:, 0] == 0) & (y[:, 0] == 0))
+        zero0 = ((x[:, 1] + y[:, 1]) & 0xFFFFFFFF) == 0
+        idx = torch.nonzero(~(zero0 & zero1)).flatten()
+        nonzero += [c0 + int(i) for i in idx[:8].cpu()]
+        # the u32 slot's padding word stays zero, the IntModN share is < p
+        assert not bool(((x[:, 1] >> 32) != 0).any()), c0
+        assert not bool((((x[:, 0] < 0) & (x[:, 0] >= -59))).any()), c0
+    assert nonzero == [alpha]
+    xa = [int(v) & 0xFFFFFFFFFFFFFFFF for v in a[alpha].cpu()]
+    xb = [int(v) & 0xFFFFFFFFFFFFFFFF for v in b[alpha].cpu()]
+    beta0, beta1 = c5_full["beta"]
+    assert (xa[1] + xb[1]) % (1 << 32) == beta0
+    assert (xa[0] + xb[0]) % P64 == beta1
+
+
+def test_c5_full_domain_sampled_subtrees_match_oracle(c5_full):
+    """First, last, alpha's and 5 seeded random 2^20-leaf subtrees of both
+    parties' 2^32-leaf launches equal the oracle's expansion bit for bit."""
+    d, alpha = c5_full["d"], c5_full["alpha"]
+    log_blocks = 20
+    nsub = c5_full["n"] >> log_blocks
+    rng = random.Random(2032)
+    subs = sorted({0, nsub - 1, alpha >> log_blocks} | {rng.randrange(nsub) for _ in range(5)})
+    for party, key in enumerate(c5_full["keys"]):
+        out = c5_full["outs"][party]
+        for s in subs:
+            first = s << log_blocks
+            want = d.expand_subtree_words(key, first, log_blocks).reshape(-1, 2, 2)
+            got = out[first * 16:(first + (1 << log_blocks)) * 16].cpu().numpy()
+            _assert_host_layout_equals_words(C5, got, want, "party %d subtree %d" % (party, s))
+
+
+def test_c5_leaf_ranges_above_2_31_equal_full_launch(K, cuda, c5_full):
+    """Leaf-range launches (the sharded entry) beginning past 2^31 produce
+    exactly the corresponding slice of the full launch; one is also checked
+    against the oracle."""
+    import torch
+    d, key = c5_full["d"], c5_full["keys"][0]
+    full = c5_full["outs"][0]
+    rng = random.Random(31)
+    ranges = [((1 << 31) + 12345, (1 << 31) + 12345 + (1 << 21) + 7),
+              ((1 << 32) - (1 << 22) - 1, 1 << 32),
+              ((1 << 31), (1 << 31) + 1)]
+    for _ in range(2):
+        lo = (1 << 31) + rng.randrange(1 << 30)
+        ranges.append((lo, lo + rng.randrange(1, 1 << 22)))
+    for lo, hi in ranges:
+        got = _expand(K, cuda, d, key, C5, lo, hi)
+        assert torch.equal(got, full[lo * 16:hi * 16]), (lo, hi)
+    lo, hi = ranges[0]
+    first = lo >> 20 << 20
+    want = d.expand_subtree_words(key, first, 22).reshape(-1, 2, 2)[lo - first:hi - first]
+    got = _expand(K, cuda, d, key, C5, lo, hi).cpu().numpy()
+    _assert_host_layout_equals_words(C5, got, want, "range above 2^31")
+
+
+def test_c5_eight_rank_split_reproduces_one_rank(K, cuda, c5_full):
+    """bench.py's N = 8 split (sharding.block_range over 2^32 tree blocks),
+    each rank's launch run in turn on this GPU into its slice of one buffer,
+    equals the single-rank output byte for byte."""
+    import torch
+    from distributed_point_functions_amd import sharding
+    d, key, n = c5_full["d"], c5_full["keys"][0], c5_full["n"]
+    full = c5_full["outs"][0]
+    # reuse party 1's buffer (its checks ran first in this module)
+    buf = c5_full["outs"][1]
+    for world in (8, 3):
+        for rank in range(world):
+            lo, hi = sharding.block_range(n, world, rank)
+            _expand(K, cuda, d, key, C5, lo, hi, out=buf[lo * 16:hi * 16])
+        assert _chunked_equal(buf, full), world
