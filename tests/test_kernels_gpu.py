@@ -309,7 +309,11 @@ def test_gather_rows(K, cuda, stride, opp):
 
 @pytest.mark.parametrize("n,size,q", [(1, 16, 1), (1000, 256, 1), (1000, 256, 3),
                                       (4096, 80, 8), (300, 17, 2), (777, 1104, 5),
-                                      (129, 4096, 1), (5000, 64, 11)])
+                                      (129, 4096, 1), (5000, 64, 11),
+                                      # many-query (Four Russians) scan: > 16 queries,
+                                      # records a multiple of 256 B
+                                      (1000, 256, 17), (3001, 256, 32), (4097, 512, 33),
+                                      (130, 256, 64), (2500, 768, 100)])
 def test_inner_product_matches_oracle(K, cuda, n, size, q):
     import torch
     rng = np.random.default_rng(n * 7 + size)

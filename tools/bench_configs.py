@@ -263,7 +263,7 @@ def c4q(dev, reps):
     gen.manual_seed(4)
     db = torch.randint(0, 256, (n * rec,), dtype=torch.uint8, device=dev, generator=gen)
     res = {"config": "c4q", "workload": "XOR scan 2^26 x 256 B"}
-    for q in (1, 8, 64):
+    for q in (1, 8, 16, 32, 64, 100):
         sel = torch.randint(-2**63, 2**63 - 1, (q * (n // 128), 2), dtype=torch.int64,
                             device=dev, generator=gen)
         ws = torch.empty(max(16, _lib.lib().dpf_amd_inner_product_workspace_size(n, rec, q)),

@@ -1,0 +1,682 @@
+"""EXPERIMENT (not in the library).  Generates
+tools/experiments/bsaes_gen.h: a bitsliced
+AES-128 for gfx950 with the DPF value-PRG key (dpf/distributed_point_
+function.cc:55-60, kPrgKeyValue) compiled into the circuit, 32 blocks per
+lane (one block per bit of a 32-bit VGPR), expressed in v_bitop3_b32
+(any 3-input boolean function in one VALU op) and v_perm_b32.
+
+    python tools/gen_bsaes.py            # writes the header, verifies it
+
+Why: the T-table AES of the fused expansion kernel is bound by LDS lookup
+issue (~90 % of LDS-array cycles) while the VALU idles at ~45 % (DESIGN.md
+§3.1).  A bitsliced AES uses no LDS at all, so computing the value-PRG
+blocks of some leaves bitsliced moves work from the saturated LDS pipe onto
+the idle VALU.
+
+Construction:
+  * S-box: the Boyar-Peralta depth-16 circuit (J. Boyar, R. Peralta, "A
+    depth-16 circuit for the AES S-box", 2011: 34 AND + 94 XOR/XNOR),
+    checked against the AES S-box table below;
+  * each output column of a round (four S-boxes + MixColumns) is one
+    XOR/AND DAG, technology-mapped onto 3-input LUTs (cut enumeration +
+    area flow + exact-area recovery): every LUT is one v_bitop3_b32;
+  * AddRoundKey costs nothing: the round keys are compile-time constants, so
+    a key bit of 1 is an inverted LUT input (folded into the LUT's truth
+    table); ShiftRows is renaming; the last round key is folded into the
+    Matyas-Meyer-Oseas XOR after the output transpose;
+  * transposes between the word layout and the bitsliced layout are the
+    5-stage block-swap transpose (v_perm_b32 for the 16- and 8-bit stages).
+    Input block i and i + 16 are sigma(s_i) and sigma(s_i + 1) of an even
+    seed s_i (the value-PRG pair of a 160-bit type, cc:533-537): they differ
+    only in bit 64, so the 16-bit stage is a byte duplication.
+The emitted op stream is simulated here and compared with a reference
+AES-MMO on random seeds before the header is written.
+"""
+from __future__ import annotations
+
+import os
+import random
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+OUT = os.path.join(ROOT, "tools", "experiments", "bsaes_gen.h")
+
+BARRIERS = os.environ.get("BSAES_BARRIERS", "1") == "1"
+# measurement only: fewer middle rounds (wrong results) to probe code-size effects
+EXPERIMENT_ROUNDS = int(os.environ.get("BSAES_ROUNDS", "9"))
+ORDER = os.environ.get("BSAES_ORDER", "rr")
+KEY_VALUE = (0x05a5d1588c5423e3 << 64) | 0x46a31101b21d1c98  # cc:55-60
+
+# --------------------------------------------------------------------------
+# Reference AES-128 (FIPS-197) for verification.
+# --------------------------------------------------------------------------
+
+
+def _gmul(a, b):
+    p = 0
+    for _ in range(8):
+        if b & 1:
+            p ^= a
+        hi = a & 0x80
+        a = (a << 1) & 0xFF
+        if hi:
+            a ^= 0x1B
+        b >>= 1
+    return p
+
+
+def _sbox():
+    inv = [0] * 256
+    for x in range(1, 256):
+        for y in range(1, 256):
+            if _gmul(x, y) == 1:
+                inv[x] = y
+                break
+    out = []
+    for x in range(256):
+        b = inv[x]
+        s = b
+        for i in range(1, 5):
+            s ^= ((b << i) | (b >> (8 - i))) & 0xFF
+        out.append(s ^ 0x63)
+    return out
+
+
+SBOX = _sbox()
+
+
+def expand_key(key: int):
+    """11 round keys as 16-byte lists; key bytes = little-endian bytes of the
+    uint128 (aes_128_fixed_key_hash.cc:50)."""
+    w = [list(key.to_bytes(16, "little")[4 * i:4 * i + 4]) for i in range(4)]
+    rcon = 1
+    for i in range(4, 44):
+        t = list(w[i - 1])
+        if i % 4 == 0:
+            t = t[1:] + t[:1]
+            t = [SBOX[x] for x in t]
+            t[0] ^= rcon
+            rcon = _gmul(rcon, 2)
+        w.append([a ^ b for a, b in zip(w[i - 4], t)])
+    return [sum(w[4 * r:4 * r + 4], []) for r in range(11)]
+
+
+def aes_encrypt(rks, block: bytes) -> bytes:
+    s = [b ^ k for b, k in zip(block, rks[0])]
+    for r in range(1, 11):
+        s = [SBOX[x] for x in s]
+        s = [s[i % 4 + 4 * ((i // 4 + i % 4) % 4)] for i in range(16)]  # ShiftRows
+        if r < 10:
+            t = []
+            for c in range(4):
+                a = s[4 * c:4 * c + 4]
+                for i in range(4):
+                    t.append(_gmul(a[i], 2) ^ _gmul(a[(i + 1) % 4], 3) ^ a[(i + 2) % 4] ^
+                             a[(i + 3) % 4])
+            s = t
+        s = [b ^ k for b, k in zip(s, rks[r])]
+    return bytes(s)
+
+
+def sigma(x: int) -> int:
+    lo, hi = x & ((1 << 64) - 1), x >> 64
+    return ((hi ^ lo) << 64) | hi
+
+
+def mmo(rks, x: int) -> int:
+    s = sigma(x)
+    return int.from_bytes(aes_encrypt(rks, s.to_bytes(16, "little")), "little") ^ s
+
+
+# --------------------------------------------------------------------------
+# Circuits and LUT mapping.
+# --------------------------------------------------------------------------
+
+BP_SBOX = """
+T1=U0^U3 T2=U0^U5 T3=U0^U6 T4=U3^U5 T5=U4^U6 T6=T1^T5 T7=U1^U2 T8=U7^T6 T9=U7^T7
+T10=T6^T7 T11=U1^U5 T12=U2^U5 T13=T3^T4 T14=T6^T11 T15=T5^T11 T16=T5^T12 T17=T9^T16
+T18=U3^U7 T19=T7^T18 T20=T1^T19 T21=U6^U7 T22=T7^T21 T23=T2^T22 T24=T2^T10 T25=T20^T17
+T26=T3^T16 T27=T1^T12
+M1=T13&T6 M2=T23&T8 M3=T14^M1 M4=T19&U7 M5=M4^M1 M6=T3&T16 M7=T22&T9 M8=T26^M6
+M9=T20&T17 M10=M9^M6 M11=T1&T15 M12=T4&T27 M13=M12^M11 M14=T2&T10 M15=M14^M11
+M16=M3^M2 M17=M5^T24 M18=M8^M7 M19=M10^M15 M20=M16^M13 M21=M17^M15 M22=M18^M13
+M23=M19^T25 M24=M22^M23 M25=M22&M20 M26=M21^M25 M27=M20^M21 M28=M23^M25 M29=M28&M27
+M30=M26&M24 M31=M20&M23 M32=M27&M31 M33=M27^M25 M34=M21&M22 M35=M24&M34 M36=M24^M25
+M37=M21^M29 M38=M32^M33 M39=M23^M30 M40=M35^M36 M41=M38^M40 M42=M37^M39 M43=M37^M38
+M44=M39^M40 M45=M42^M41 M46=M44&T6 M47=M40&T8 M48=M39&U7 M49=M43&T16 M50=M38&T9
+M51=M37&T17 M52=M42&T15 M53=M45&T27 M54=M41&T10 M55=M44&T13 M56=M40&T23 M57=M39&T19
+M58=M43&T3 M59=M38&T22 M60=M37&T20 M61=M42&T1 M62=M45&T4 M63=M41&T2
+L0=M61^M62 L1=M50^M56 L2=M46^M48 L3=M47^M55 L4=M54^M58 L5=M49^M61 L6=M62^L5 L7=M46^L3
+L8=M51^M59 L9=M52^M53 L10=M53^L4 L11=M60^L2 L12=M48^M51 L13=M50^L0 L14=M52^M61
+L15=M55^L1 L16=M56^L0 L17=M57^L1 L18=M58^L8 L19=M63^L4 L20=L0^L1 L21=L1^L7 L22=L3^L12
+L23=L18^L2 L24=L15^L9 L25=L6^L10 L26=L7^L9 L27=L8^L10 L28=L11^L14 L29=L11^L17
+S0=L6^L24 S1=L16~L26 S2=L19~L28 S3=L6^L21 S4=L20^L22 S5=L25^L29 S6=L13~L27 S7=L6~L23
+"""  # U0 / S0 = most significant bit; a~b = XNOR
+
+
+class Circ:
+    def __init__(self):
+        self.nodes = {}  # name -> (op, a, b); op in in / xor / xnor / and
+        self.order = []
+
+    def inp(self, n):
+        self.nodes[n] = ("in", None, None)
+        self.order.append(n)
+        return n
+
+    def gate(self, n, op, a, b):
+        assert n not in self.nodes, n
+        self.nodes[n] = (op, a, b)
+        self.order.append(n)
+        return n
+
+    def is_in(self, n):
+        return self.nodes[n][0] == "in"
+
+
+def add_sbox(c: Circ, u, pfx):
+    """u: 8 input names, MSB first; returns the 8 output names, MSB first."""
+    env = {"U%d" % i: u[i] for i in range(8)}
+    for tok in BP_SBOX.split():
+        lhs, rhs = tok.split("=")
+        for op, sym in (("xor", "^"), ("xnor", "~"), ("and", "&")):
+            if sym in rhs:
+                a, b = rhs.split(sym)
+                env[lhs] = c.gate(pfx + lhs, op, env[a], env[b])
+                break
+    return [env["S%d" % i] for i in range(8)]
+
+
+def xtime_terms(a, j):
+    """bit j of xtime(a) as a list of bits of a (LSB-first names)."""
+    return {0: [a[7]], 1: [a[0], a[7]], 2: [a[1]], 3: [a[2], a[7]], 4: [a[3], a[7]],
+            5: [a[4]], 6: [a[5]], 7: [a[6]]}[j]
+
+
+def column_circuit(mix: bool):
+    """Inputs x{r}_{b} (row r, bit b LSB-first) of the four bytes feeding one
+    output column; outputs 32 bits (row-major, LSB-first)."""
+    c = Circ()
+    ins = [[c.inp("x%d_%d" % (r, b)) for b in range(8)] for r in range(4)]
+    a = [add_sbox(c, ins[r][::-1], "s%d_" % r)[::-1] for r in range(4)]
+    if not mix:
+        return c, ins, [a[r][b] for r in range(4) for b in range(8)]
+    cnt = [0]
+
+    def X(x, y):
+        cnt[0] += 1
+        return c.gate("g%d" % cnt[0], "xor", x, y)
+
+    def xor_list(lst):
+        lst = list(lst)
+        while len(lst) > 1:
+            nxt = [X(lst[i], lst[i + 1]) for i in range(0, len(lst) - 1, 2)]
+            if len(lst) % 2:
+                nxt.append(lst[-1])
+            lst = nxt
+        return lst[0]
+    # b_i = xtime(a_i ^ a_{i+1}) ^ a_{i+1} ^ (a_{i+2} ^ a_{i+3})
+    d = [[X(a[i][j], a[(i + 1) % 4][j]) for j in range(8)] for i in range(4)]
+    outs = []
+    for i in range(4):
+        for j in range(8):
+            outs.append(xor_list(xtime_terms(d[i], j) + [a[(i + 1) % 4][j], d[(i + 2) % 4][j]]))
+    return c, ins, outs
+
+
+def enum_cuts(c: Circ, K=3):
+    cuts = {}
+    for n in c.order:
+        op, a, b = c.nodes[n]
+        s = {frozenset([n])}
+        if op != "in":
+            for x in cuts[a]:
+                for y in cuts[b]:
+                    u = x | y
+                    if len(u) <= K:
+                        s.add(u)
+        keep = []
+        for x in sorted(s, key=len):
+            if not any(y < x for y in keep):
+                keep.append(x)
+        cuts[n] = keep
+    return cuts
+
+
+def map_luts(c: Circ, outputs, K=3, iters=6):
+    """Area-oriented 3-LUT cover: area flow, then exact-area recovery."""
+    cuts = enum_cuts(c, K)
+    fo = {n: 0 for n in c.order}
+    for n in c.order:
+        op, a, b = c.nodes[n]
+        if op != "in":
+            fo[a] += 1
+            fo[b] += 1
+    for o in outputs:
+        fo[o] += 1
+    af, cut = {}, {}
+    for n in c.order:
+        if c.is_in(n):
+            af[n] = 0
+            continue
+        best = None
+        for ct in cuts[n]:
+            if ct == frozenset([n]):
+                continue
+            v = 1 + sum(af[l] / max(1, fo[l]) for l in ct)
+            if best is None or v < best[0] - 1e-9:
+                best = (v, ct)
+        af[n], cut[n] = best
+    refs = {n: 0 for n in c.order}
+
+    def deref(n):
+        area = 1
+        for l in cut[n]:
+            refs[l] -= 1
+            if refs[l] == 0 and not c.is_in(l):
+                area += deref(l)
+        return area
+
+    def ref(n):
+        area = 1
+        for l in cut[n]:
+            if refs[l] == 0 and not c.is_in(l):
+                area += ref(l)
+            refs[l] += 1
+        return area
+    for o in outputs:
+        if refs[o] == 0 and not c.is_in(o):
+            ref(o)
+        refs[o] += 1
+    for _ in range(iters):
+        for n in c.order:
+            if c.is_in(n) or refs[n] == 0:
+                continue
+            deref(n)
+            best = None
+            for ct in cuts[n]:
+                if ct == frozenset([n]):
+                    continue
+                cut[n] = ct
+                area = ref(n)
+                deref(n)
+                if best is None or area < best[0]:
+                    best = (area, ct)
+            cut[n] = best[1]
+            ref(n)
+    return [(n, sorted(cut[n])) for n in c.order if not c.is_in(n) and refs[n] > 0]
+
+
+def node_value(c: Circ, n, assign, memo):
+    if n in assign:
+        return assign[n]
+    if n in memo:
+        return memo[n]
+    op, a, b = c.nodes[n]
+    x, y = node_value(c, a, assign, memo), node_value(c, b, assign, memo)
+    v = x ^ y if op == "xor" else (1 ^ x ^ y if op == "xnor" else x & y)
+    memo[n] = v
+    return v
+
+
+# v_bitop3_b32 truth table: result bit = TT[(a << 2) | (b << 1) | c], i.e.
+# TT = f(0xF0, 0xCC, 0xAA) evaluated bitwise (LLVM AMDGPU BitOp3 encoding).
+SRC_BITS = (0xF0, 0xCC, 0xAA)
+
+
+def lut_tt(c: Circ, n, leaves, inverted):
+    """Truth table of node n over up to 3 leaves (leaf value = register value
+    ^ inverted[leaf])."""
+    tt = 0
+    for i in range(8):
+        bits = [(i >> (2 - k)) & 1 for k in range(3)]  # a = bit 2 of the index
+        assign = {l: bits[k] ^ inverted.get(l, 0) for k, l in enumerate(leaves)}
+        if node_value(c, n, assign, {}):
+            tt |= 1 << i
+    return tt
+
+
+# --------------------------------------------------------------------------
+# Op stream: SSA values, each op is (dst, kind, args).
+# --------------------------------------------------------------------------
+
+class Prog:
+    def __init__(self):
+        self.ops = []
+        self.n = 0
+
+    def new(self):
+        self.n += 1
+        return "v%d" % self.n
+
+    def bitop3(self, a, b, cc, tt):
+        d = self.new()
+        self.ops.append((d, "bitop3", (a, b, cc, tt)))
+        return d
+
+    def perm(self, a, b, sel):
+        d = self.new()
+        self.ops.append((d, "perm", (a, b, sel)))
+        return d
+
+    def shl(self, a, s):
+        d = self.new()
+        self.ops.append((d, "shl", (a, s)))
+        return d
+
+    def shr(self, a, s):
+        d = self.new()
+        self.ops.append((d, "shr", (a, s)))
+        return d
+
+    def barrier(self):
+        self.ops.append((None, "barrier", ()))
+
+    def xor_k(self, a, k):  # a ^ 32-bit constant
+        d = self.new()
+        self.ops.append((d, "xork", (a, k)))
+        return d
+
+    def xor3k(self, a, b, k):  # a ^ b ^ 32-bit constant
+        d = self.new()
+        self.ops.append((d, "xor3k", (a, b, k)))
+        return d
+
+
+MASKS = {4: 0x0F0F0F0F, 2: 0x33333333, 1: 0x55555555}
+
+
+def transpose_stage(p: Prog, R, j, need=None):
+    """One block-swap stage (rows p, p + j exchange their j-bit halves).
+    need: optional set of row indices whose new value is wanted."""
+    out = list(R)
+    for a in range(32):
+        if a & j:
+            continue
+        q = a + j
+        want_a = need is None or a in need
+        want_q = need is None or q in need
+        if j == 16:
+            if want_a:
+                out[a] = p.perm(R[q], R[a], 0x05040100)
+            if want_q:
+                out[q] = p.perm(R[q], R[a], 0x07060302)
+        elif j == 8:
+            if want_a:
+                out[a] = p.perm(R[q], R[a], 0x06020400)
+            if want_q:
+                out[q] = p.perm(R[q], R[a], 0x07030501)
+        else:
+            m = MASKS[j]
+            if want_a:
+                out[a] = p.bitop3(R[a], p.shl(R[q], j), "K%08x" % m, 0xE4)
+            if want_q:
+                out[q] = p.bitop3(p.shr(R[a], j), R[q], "K%08x" % m, 0xE4)
+    return out
+
+
+def generate():
+    rks = expand_key(KEY_VALUE)
+    key_bit = lambda r, byte, b: (rks[r][byte] >> b) & 1  # noqa: E731
+    p = Prog()
+    # inputs: sg[i][c] = word c of sigma(s_i), i < 16
+    sg = [["sg[%d][%d]" % (i, c) for c in range(4)] for i in range(16)]
+    # ---- input transpose, column by column: rows b = blocks (b, b + 16
+    # identical), 16-bit stage first (byte duplication), then 8, 4, 2, 1.
+    slices = {}
+    for c in range(4):
+        R = [None] * 32
+        for i in range(16):
+            R[i] = p.perm(sg[i][c], sg[i][c], 0x01000100)       # low half twice
+            R[i + 16] = p.perm(sg[i][c], sg[i][c], 0x03020302)  # high half twice
+        for j in (8, 4, 2, 1):
+            R = transpose_stage(p, R, j)
+        for k in range(32):
+            slices[32 * c + k] = R[k]
+    # odd blocks (bits 16..31) = sigma(s_i + 1): bit 64 (word 2, bit 0) flips
+    slices[64] = p.xor_k(slices[64], 0xFFFF0000)
+    # state[(row, col)] = 8 SSA names, LSB first; slice = word col, bit 8 row + b
+    state = {(r, col): [slices[32 * col + 8 * r + b] for b in range(8)]
+             for r in range(4) for col in range(4)}
+    key_in = {(r, col): [key_bit(0, 4 * col + r, b) for b in range(8)]
+              for r in range(4) for col in range(4)}
+    maps = {}
+    for mix in (True, False):
+        circ, ins, outs = column_circuit(mix)
+        maps[mix] = (circ, ins, outs, map_luts(circ, outs))
+    for rnd in list(range(1, 1 + EXPERIMENT_ROUNDS)) + [10]:
+        mix = rnd < 10
+        circ, ins, outs, luts = maps[mix]
+        new_state = {}
+        for col in range(4):
+            src = [((r, (col + r) % 4)) for r in range(4)]  # ShiftRows
+            env, inv = {}, {}
+            for r in range(4):
+                for b in range(8):
+                    env[ins[r][b]] = state[src[r]][b]
+                    inv[ins[r][b]] = key_in[src[r]][b]
+            group = None
+            for n, leaves in emission_order(luts):
+                g = n.split("_")[0] if "_" in n else "mix"
+                if ORDER == "seq" and g != group:  # one S-box at a time
+                    p.barrier()
+                    group = g
+                tt = lut_tt(circ, n, leaves, inv)
+                args = [env[l] for l in leaves]
+                if len(leaves) < 3:  # unused operands repeat the first leaf
+                    args += [args[0]] * (3 - len(leaves))
+                    tt = _padded_tt(circ, n, leaves, inv)
+                env[n] = p.bitop3(args[0], args[1], args[2], tt)
+            if ORDER != "seq":
+                p.barrier()
+            for r in range(4):
+                new_state[(r, col)] = [env[outs[8 * r + b]] for b in range(8)]
+        state = new_state
+        if rnd < 10:
+            key_in = {(r, col): [key_bit(rnd, 4 * col + r, b) for b in range(8)]
+                      for r in range(4) for col in range(4)}
+    # ---- output transpose; the last round key and the MMO XOR with sigma
+    # are applied in the word domain.  Wanted: words 0..3 of blocks 0..15,
+    # word 0 of blocks 16..31.
+    result = {}
+    for c in range(4):
+        R = [state[(k // 8, c)][k % 8] for k in range(32)]
+        for j in (1, 2, 4, 8):
+            R = transpose_stage(p, R, j)
+        need = set(range(32)) if c == 0 else set(range(16))
+        R = transpose_stage(p, R, 16, need)
+        for i in sorted(need):
+            result[(i, c)] = R[i]
+    return p, result
+
+
+def last_round_key_words():
+    rks = expand_key(KEY_VALUE)
+    return [int.from_bytes(bytes(rks[10][4 * c:4 * c + 4]), "little") for c in range(4)]
+
+
+def emission_order(luts):
+    """seq: S-box by S-box, then MixColumns.  rr: the four S-boxes of a
+    column interleaved LUT by LUT (four independent dependency chains for
+    the issue stream), then MixColumns."""
+    if ORDER == "seq":
+        return luts
+    groups = {}
+    for item in luts:
+        g = item[0].split("_")[0] if "_" in item[0] else "mix"
+        groups.setdefault(g, []).append(item)
+    sb = [groups.get("s%d" % r, []) for r in range(4)]
+    out = []
+    for i in range(max(len(x) for x in sb)):
+        for x in sb:
+            if i < len(x):
+                out.append(x[i])
+    return out + groups.get("mix", [])
+
+
+def _padded_tt(circ, n, leaves, inv):
+    """Truth table when the LUT has < 3 leaves: unused operands repeat the
+    first leaf, so only indices with equal bits for those operands matter."""
+    k = len(leaves)
+    tt = 0
+    for i in range(8):
+        bits = [(i >> (2 - m)) & 1 for m in range(3)]
+        if any(bits[m] != bits[0] for m in range(k, 3)):
+            continue  # unreachable combination
+        assign = {l: bits[m] ^ inv.get(l, 0) for m, l in enumerate(leaves)}
+        if node_value(circ, n, assign, {}):
+            tt |= 1 << i
+    return tt
+
+
+# --------------------------------------------------------------------------
+# Simulation of the op stream and verification.
+# --------------------------------------------------------------------------
+
+M32 = 0xFFFFFFFF
+
+
+def simulate(p: Prog, result, sg_words):
+    env = {}
+    for i in range(16):
+        for c in range(4):
+            env["sg[%d][%d]" % (i, c)] = sg_words[i][c]
+
+    def val(x):
+        if isinstance(x, str) and x.startswith("K"):
+            return int(x[1:], 16)
+        return env[x]
+    for d, kind, args in p.ops:
+        if kind == "bitop3":
+            a, b, cc, tt = args
+            a, b, cc = val(a), val(b), val(cc)
+            r = 0
+            for bit in range(32):
+                idx = (((a >> bit) & 1) << 2) | (((b >> bit) & 1) << 1) | ((cc >> bit) & 1)
+                r |= ((tt >> idx) & 1) << bit
+            env[d] = r
+        elif kind == "perm":
+            a, b, sel = val(args[0]), val(args[1]), args[2]
+            pool = (a << 32) | b
+            r = 0
+            for i in range(4):
+                s = (sel >> (8 * i)) & 0xFF
+                byte = (pool >> (8 * s)) & 0xFF if s < 8 else (0 if s == 12 else 0xFF)
+                r |= byte << (8 * i)
+            env[d] = r
+        elif kind == "shl":
+            env[d] = (val(args[0]) << args[1]) & M32
+        elif kind == "shr":
+            env[d] = val(args[0]) >> args[1]
+        elif kind == "xork":
+            env[d] = val(args[0]) ^ args[1]
+        elif kind == "xor3k":
+            env[d] = val(args[0]) ^ val(args[1]) ^ args[2]
+        elif kind == "barrier":
+            pass
+    return {k: env[v] for k, v in result.items()}
+
+
+def verify(p, result, trials=3):
+    # the reference AES-MMO itself against the reference KAT
+    # (dpf/aes_128_fixed_key_hash_test.cc:120-141)
+    seed0 = (0x0123012301230123 << 64) | 0x0123012301230123
+    assert mmo(expand_key(0), seed0) == (0x73c2dc14812be4ef << 64) | 0xeac64d09c8adf8ed
+    rks = expand_key(KEY_VALUE)
+    rng = random.Random(1)
+    for _ in range(trials):
+        seeds = [rng.getrandbits(128) & ~1 for _ in range(16)]
+        sgw = []
+        for s in seeds:
+            x = sigma(s)
+            sgw.append([(x >> (32 * c)) & M32 for c in range(4)])
+        got = simulate(p, result, sgw)
+        k10 = last_round_key_words()
+        got = {(i, c): v ^ sgw[i % 16][c] ^ k10[c] for (i, c), v in got.items()}
+        for i, s in enumerate(seeds):
+            h0 = mmo(rks, s)
+            h1 = mmo(rks, s + 1)
+            for c in range(4):
+                assert got[(i, c)] == (h0 >> (32 * c)) & M32, (i, c)
+            assert got[(i + 16, 0)] == h1 & M32, i
+
+
+# --------------------------------------------------------------------------
+# C++ emission.
+# --------------------------------------------------------------------------
+
+def emit(p: Prog, result) -> str:
+    counts = {}
+    for _, kind, _ in p.ops:
+        if kind != "barrier":
+            counts[kind] = counts.get(kind, 0) + 1
+    nops = sum(counts.values())
+    lines = []
+    w = lines.append
+    w("// Generated by tools/gen_bsaes.py -- do not edit.")
+    w("// Bitsliced AES-128-MMO with the DPF value key (cc:55-60) for 16 value-PRG")
+    w("// pairs (sigma(s_i), sigma(s_i + 1)) of even seeds s_i, 32 blocks per lane.")
+    w("// Ops: " + ", ".join("%s %d" % kv for kv in sorted(counts.items())) +
+      " (VALU ops per lane: %d, per block: %.1f)" % (nops, nops / 32.0))
+    w("#pragma once")
+    w("#include <cstdint>")
+    w("namespace dpf_amd {")
+    k10 = last_round_key_words()
+    w("// Last round key words: H = AES(sigma) ^ sigma = out ^ sigma ^ kBsK10.")
+    w("constexpr uint32_t kBsK10[4] = {" + ", ".join("0x%08xu" % k for k in k10) + "};")
+    w("// sg[i][c]: word c of sigma(s_i) (read by the input transpose only).")
+    w("// Outputs (before the Matyas-Meyer-Oseas XOR and the last round key):")
+    w("// w0[i][c]: word c of AES rounds 0-9 + SubBytes/ShiftRows of sigma(s_i);")
+    w("// w1[i]: word 0 of the same for sigma(s_i + 1).  Finish with")
+    w("// H(s_i)[c] = w0[i][c] ^ sg[i][c] ^ kBsK10[c], H(s_i + 1)[0] = w1[i] ^ sg[i][0] ^ kBsK10[0].")
+    w("__device__ __forceinline__ void BsAesPairs16(const uint32_t (&sg)[16][4],")
+    w("                                             uint32_t (&w0)[16][4],")
+    w("                                             uint32_t (&w1)[16]) {")
+    consts = sorted({a for _, _, args in p.ops for a in args
+                     if isinstance(a, str) and a.startswith("K")})
+    for k in consts:
+        w("  const uint32_t %s = 0x%su;" % (k, k[1:]))
+    for d, kind, args in p.ops:
+        if kind == "bitop3":
+            w("  const uint32_t %s = __builtin_amdgcn_bitop3_b32(%s, %s, %s, 0x%02x);" %
+              (d, args[0], args[1], args[2], args[3]))
+        elif kind == "perm":
+            w("  const uint32_t %s = __builtin_amdgcn_perm(%s, %s, 0x%08xu);" %
+              (d, args[0], args[1], args[2]))
+        elif kind == "shl":
+            w("  const uint32_t %s = %s << %d;" % (d, args[0], args[1]))
+        elif kind == "shr":
+            w("  const uint32_t %s = %s >> %d;" % (d, args[0], args[1]))
+        elif kind == "xork":
+            w("  const uint32_t %s = %s ^ 0x%08xu;" % (d, args[0], args[1]))
+        elif kind == "xor3k":
+            w("  const uint32_t %s = __builtin_amdgcn_bitop3_b32(%s, %s, 0x%08xu, 0x96);" %
+              (d, args[0], args[1], args[2]))
+        elif kind == "barrier" and BARRIERS:
+            w("  __builtin_amdgcn_sched_barrier(0);")
+    for (i, c), v in sorted(result.items()):
+        if i < 16:
+            w("  w0[%d][%d] = %s;" % (i, c, v))
+        else:
+            w("  w1[%d] = %s;" % (i - 16, v))
+    w("}")
+    w("}  // namespace dpf_amd")
+    return "\n".join(lines) + "\n"
+
+
+def main():
+    p, result = generate()
+    if EXPERIMENT_ROUNDS == 9:
+        verify(p, result)
+    if len(sys.argv) > 1:
+        global OUT
+        OUT = sys.argv[1]
+    text = emit(p, result)
+    with open(OUT, "w") as f:
+        f.write(text)
+    print("wrote %s: %d ops (%.1f per block); verified against reference AES-MMO" %
+          (OUT, len(p.ops), len(p.ops) / 32.0))
+
+
+if __name__ == "__main__":
+    sys.exit(main())
