@@ -119,6 +119,8 @@ def _bind_tier2(L):
     _sig(L, "dpf_amd_dpf_tree_levels_needed", I32, P)
     _sig(L, "dpf_amd_dpf_hierarchy_to_tree", I32, P, I32)
     _sig(L, "dpf_amd_dpf_value_type", I32, P, I32, ctypes.POINTER(ValueTypeDesc))
+    _sig(L, "dpf_amd_dpf_register_value_type", I32, P, P, SZ)
+    _sig(L, "dpf_amd_dcf_register_value_type", I32, P, P, SZ)
     _sig(L, "dpf_amd_dpf_generate_keys", I32, P, U64, U64, P, P, P, BUF,
          ctypes.POINTER(SZ), BUF, ctypes.POINTER(SZ))
     _sig(L, "dpf_amd_ctx_create", I32, P, P, SZ, PP)

@@ -117,6 +117,26 @@ int dpf_amd_dpf_value_type(const dpf_amd_dpf* dpf, int level, dpf_amd_value_type
   return DPF_AMD_OK;
 }
 
+int dpf_amd_dpf_register_value_type(dpf_amd_dpf* dpf, const uint8_t* value_type_proto,
+                                    size_t len) {
+  if (!dpf) return Fail(DPF_AMD_INVALID_ARGUMENT, "null handle");
+  ValueType vt;
+  if (!ParseValueType(value_type_proto, len, &vt))
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed ValueType proto");
+  Status s = dpf->dpf->RegisterValueTypeProto(vt);
+  return s.ok() ? DPF_AMD_OK : Fail(s);
+}
+
+int dpf_amd_dcf_register_value_type(dpf_amd_dcf* dcf, const uint8_t* value_type_proto,
+                                    size_t len) {
+  if (!dcf) return Fail(DPF_AMD_INVALID_ARGUMENT, "null handle");
+  ValueType vt;
+  if (!ParseValueType(value_type_proto, len, &vt))
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed ValueType proto");
+  Status s = const_cast<DistributedPointFunction&>(dcf->dcf->dpf()).RegisterValueTypeProto(vt);
+  return s.ok() ? DPF_AMD_OK : Fail(s);
+}
+
 int dpf_amd_dpf_generate_keys(dpf_amd_dpf* dpf, uint64_t alpha_lo, uint64_t alpha_hi,
                               const uint8_t* const* betas, const size_t* beta_lengths,
                               const uint64_t* seeds, uint8_t** key0, size_t* key0_len,

@@ -16,6 +16,9 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <cstdio>
+#include <mutex>
+#include <set>
 #include <sstream>
 #include <unordered_map>
 
@@ -386,6 +389,11 @@ class DpfState {
   HostAes prg_left{MakeUint128(dpf_amd::kPrgKeyLeftHi, dpf_amd::kPrgKeyLeftLo)};
   HostAes prg_right{MakeUint128(dpf_amd::kPrgKeyRightHi, dpf_amd::kPrgKeyRightLo)};
   HostAes prg_value{MakeUint128(dpf_amd::kPrgKeyValueHi, dpf_amd::kPrgKeyValueLo)};
+  // Value types with a value correction function (cc:567-582): keyed by the
+  // deterministic serialization of the ValueType, as the reference's
+  // value_correction_functions_ map.
+  mutable std::mutex registry_mu;
+  std::set<std::string> registered;
 };
 
 namespace {
@@ -543,6 +551,13 @@ StatusOr<std::unique_ptr<DpfState>> MakeDpfState(Span<const DpfParameters> param
   st->parameters.assign(parameters_in.begin(), parameters_in.end());
   for (DpfParameters& p : st->parameters)
     if (p.security_parameter() == 0) p.set_security_parameter(DefaultSecurity(p));
+  // For backwards compatibility the reference registers all single unsigned
+  // integers at construction (cc:620-633).
+  for (int bits : {8, 16, 32, 64, 128}) {
+    ValueType vt;
+    vt.mutable_integer()->set_bitsize(bits);
+    st->registered.insert(SerializeValueType(vt));
+  }
   const int n = static_cast<int>(st->parameters.size());
   st->hierarchy_to_tree.resize(n);
   st->tree_to_hierarchy.assign(130, -1);
@@ -602,35 +617,99 @@ StatusOr<std::unique_ptr<DpfState>> MakeDpfState(Span<const DpfParameters> param
 using dpf_internal::DpfState;
 using dpf_internal::LevelMeta;
 
-std::string ValueType::DebugString() const {
-  std::ostringstream os;
-  switch (case_) {
-    case kInteger:
-      os << "integer { bitsize: " << integer_.bitsize() << " }\n";
+// Protobuf text format (Message::DebugString): nested messages as
+// "name {" ... "}", two-space indent, proto3 scalars omitted when zero
+// (oneof members always printed), doubles as the shortest round-trip text.
+namespace {
+
+std::string Indent(int n) { return std::string(2 * n, ' '); }
+
+std::string SimpleDtoa(double d) {
+  char buf[64];
+  snprintf(buf, sizeof(buf), "%.15g", d);
+  if (strtod(buf, nullptr) != d) snprintf(buf, sizeof(buf), "%.17g", d);
+  return buf;
+}
+
+void PrintValueInteger(const Value::Integer& v, int ind, std::ostringstream& os) {
+  if (v.value_case() == Value::Integer::kValueUint64) {
+    os << Indent(ind) << "value_uint64: " << v.value_uint64() << "\n";
+  } else if (v.value_case() == Value::Integer::kValueUint128) {
+    os << Indent(ind) << "value_uint128 {\n";
+    if (v.value_uint128().high()) os << Indent(ind + 1) << "high: " << v.value_uint128().high() << "\n";
+    if (v.value_uint128().low()) os << Indent(ind + 1) << "low: " << v.value_uint128().low() << "\n";
+    os << Indent(ind) << "}\n";
+  }
+}
+
+void PrintBitsize(const char* name, int32_t bitsize, int ind, std::ostringstream& os) {
+  os << Indent(ind) << name << " {\n";
+  if (bitsize) os << Indent(ind + 1) << "bitsize: " << bitsize << "\n";
+  os << Indent(ind) << "}\n";
+}
+
+void PrintValueType(const ValueType& vt, int ind, std::ostringstream& os) {
+  switch (vt.type_case()) {
+    case ValueType::kInteger:
+      PrintBitsize("integer", vt.integer().bitsize(), ind, os);
       break;
-    case kXorWrapper:
-      os << "xor_wrapper { bitsize: " << integer_.bitsize() << " }\n";
+    case ValueType::kXorWrapper:
+      PrintBitsize("xor_wrapper", vt.xor_wrapper().bitsize(), ind, os);
       break;
-    case kIntModN:
-      os << "int_mod_n { base_integer { bitsize: " << int_mod_n_.base_integer().bitsize()
-         << " } }\n";
+    case ValueType::kIntModN:
+      os << Indent(ind) << "int_mod_n {\n";
+      if (vt.int_mod_n().has_base_integer())
+        PrintBitsize("base_integer", vt.int_mod_n().base_integer().bitsize(), ind + 1, os);
+      if (vt.int_mod_n().has_modulus()) {
+        os << Indent(ind + 1) << "modulus {\n";
+        PrintValueInteger(vt.int_mod_n().modulus(), ind + 2, os);
+        os << Indent(ind + 1) << "}\n";
+      }
+      os << Indent(ind) << "}\n";
       break;
-    case kTuple:
-      os << "tuple {\n";
-      for (const ValueType& e : tuple_.elements()) os << "  elements { " << e.DebugString() << "}\n";
-      os << "}\n";
+    case ValueType::kTuple:
+      os << Indent(ind) << "tuple {\n";
+      for (const ValueType& e : vt.tuple().elements()) {
+        os << Indent(ind + 1) << "elements {\n";
+        PrintValueType(e, ind + 2, os);
+        os << Indent(ind + 1) << "}\n";
+      }
+      os << Indent(ind) << "}\n";
       break;
     default:
       break;
   }
+}
+
+}  // namespace
+
+std::string ValueType::DebugString() const {
+  std::ostringstream os;
+  PrintValueType(*this, 0, os);
   return os.str();
 }
 
 std::string DpfParameters::DebugString() const {
   std::ostringstream os;
-  os << "log_domain_size: " << log_domain_size_ << "\nvalue_type {\n"
-     << value_type_.DebugString() << "}\nsecurity_parameter: " << security_parameter_ << "\n";
+  if (log_domain_size_) os << "log_domain_size: " << log_domain_size_ << "\n";
+  if (has_value_type_) {
+    os << "value_type {\n";
+    PrintValueType(value_type_, 1, os);
+    os << "}\n";
+  }
+  if (security_parameter_ != 0) os << "security_parameter: " << SimpleDtoa(security_parameter_) << "\n";
   return os.str();
+}
+
+Status DistributedPointFunction::RegisterValueTypeProto(const ValueType& value_type) {
+  std::lock_guard<std::mutex> lock(state_->registry_mu);
+  state_->registered.insert(SerializeValueType(value_type));
+  return OkStatus();
+}
+
+bool DistributedPointFunction::IsValueTypeRegistered(const ValueType& value_type) const {
+  std::lock_guard<std::mutex> lock(state_->registry_mu);
+  return state_->registered.count(SerializeValueType(value_type)) != 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -813,6 +892,14 @@ StatusOr<std::pair<DpfKey, DpfKey>> DistributedPointFunction::GenerateKeysIncrem
   const int last_ld = st.parameters.back().log_domain_size();
   if (last_ld < 128 && alpha >= (uint128{1} << last_ld))
     return InvalidArgumentError("`alpha` must be smaller than the output domain size");
+  // GetValueCorrectionFunction (cc:567-582), reached by every hierarchy
+  // level's value correction in GenerateNext / the last level.
+  for (int i = 0; i < L; ++i)
+    if (!IsValueTypeRegistered(st.parameters[i].value_type()))
+      return FailedPreconditionError(
+          "No value correction function known for the following parameters:\n" +
+          st.parameters[i].DebugString() +
+          "Did you call RegisterValueType<T>() with your value type?");
 
   std::array<DpfKey, 2> keys;
   keys[0].set_party(0);

@@ -76,6 +76,9 @@ class DistributedComparisonFunction:
     def generate_keys(self, alpha: int, beta, seeds: Optional[Sequence[int]] = None):
         """Keys for shares of `beta` on x < alpha (dcf.cc:81-111).  `seeds`
         (two 128-bit ints) replaces the CSPRNG for reproducible fixtures."""
+        if not isinstance(beta, bytes):  # templated GenerateKeys<T>: ToValue<T> registers T
+            tp = self.value_type.to_proto()
+            check(_lib.lib().dpf_amd_dcf_register_value_type(self._h, tp, len(tp)))
         b = beta if isinstance(beta, bytes) else self.value_type.value_proto(beta)
         sw = u128_words(list(seeds)) if seeds is not None else None
         k0 = ctypes.POINTER(ctypes.c_uint8)()

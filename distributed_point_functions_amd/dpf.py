@@ -194,14 +194,25 @@ class DistributedPointFunction:
         return d
 
     # -- keys ----------------------------------------------------------------
+    def register_value_type(self, value_type: ValueType) -> None:
+        """RegisterValueType<T>() (h:129-131)."""
+        tp = value_type.to_proto()
+        check(_lib.lib().dpf_amd_dpf_register_value_type(self._h, tp, len(tp)))
+
     def generate_keys(self, alpha: int, beta, seeds: Optional[Sequence[int]] = None):
         return self.generate_keys_incremental(alpha, [beta], seeds)
 
     def generate_keys_incremental(self, alpha: int, betas: Sequence,
                                   seeds: Optional[Sequence[int]] = None):
         """betas[i]: a Python value of parameters[i].value_type (or raw Value
-        proto bytes).  `seeds` (two 128-bit ints) replaces the CSPRNG for
-        reproducible fixtures only."""
+        proto bytes).  A Python value is converted like the reference's
+        templated overloads, which register its type (ToValue<T>, h:112-118);
+        raw Value bytes need the type registered (register_value_type) unless
+        it is a single unsigned integer.  `seeds` (two 128-bit ints) replaces
+        the CSPRNG for reproducible fixtures only."""
+        for p, b in zip(self.parameters, betas):
+            if not isinstance(b, bytes):
+                self.register_value_type(p.value_type)
         if len(betas) != len(self.parameters):
             protos = [b if isinstance(b, bytes) else b"" for b in betas]
         else:

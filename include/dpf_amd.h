@@ -259,6 +259,11 @@ int dpf_amd_dpf_value_type(const dpf_amd_dpf* dpf, int level,
  * Value proto for level i.  If `seeds` is non-NULL it supplies the two root
  * seeds (4 words) instead of the CSPRNG (for reproducible fixtures only).
  * Keys are returned as serialized DpfKey protos (free with dpf_amd_free). */
+/* DistributedPointFunction::RegisterValueType<T>() (h:129-131) by ValueType
+ * proto.  GenerateKeys with a Value of a type that is neither a single
+ * unsigned integer nor registered returns FAILED_PRECONDITION (cc:567-582). */
+int dpf_amd_dpf_register_value_type(dpf_amd_dpf* dpf, const uint8_t* value_type_proto,
+                                    size_t len);
 int dpf_amd_dpf_generate_keys(dpf_amd_dpf* dpf, uint64_t alpha_lo,
                               uint64_t alpha_hi, const uint8_t* const* betas,
                               const size_t* beta_lengths,
@@ -324,6 +329,11 @@ int dpf_amd_evaluate_and_apply(const dpf_amd_dpf* dpf,
 typedef struct dpf_amd_dcf dpf_amd_dcf;
 int dpf_amd_dcf_create(const uint8_t* parameters, size_t len, dpf_amd_dcf** out);
 void dpf_amd_dcf_destroy(dpf_amd_dcf* dcf);
+/* Registers a value type with the DCF's DPF (what the DCF's templated
+ * GenerateKeys<T> does through ToValue<T>, dcf/distributed_comparison_
+ * function.h:57-67). */
+int dpf_amd_dcf_register_value_type(dpf_amd_dcf* dcf, const uint8_t* value_type_proto,
+                                    size_t len);
 int dpf_amd_dcf_generate_keys(dpf_amd_dcf* dcf, uint64_t alpha_lo,
                               uint64_t alpha_hi, const uint8_t* beta,
                               size_t beta_len, const uint64_t* seeds,

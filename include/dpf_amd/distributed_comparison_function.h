@@ -28,7 +28,9 @@ class DistributedComparisonFunction {
             typename = std::enable_if_t<!std::is_convertible<T, Value>::value &&
                                         dpf_internal::is_supported_type<T>::value>>
   StatusOr<std::pair<DcfKey, DcfKey>> GenerateKeys(uint128 alpha, const T& beta) {
-    return GenerateKeys(alpha, distributed_point_functions::ToValue(beta));
+    StatusOr<Value> value = dpf_->ToValue(beta);  // registers T (dcf.h:60-67)
+    if (!value.ok()) return value.status();
+    return GenerateKeys(alpha, *value);
   }
   // As GenerateKeys with explicit root seeds instead of the CSPRNG (fixtures).
   StatusOr<std::pair<DcfKey, DcfKey>> GenerateKeysWithSeeds(uint128 alpha, const Value& beta,

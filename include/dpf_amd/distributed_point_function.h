@@ -7,8 +7,11 @@
 // Drop-in notes: names, argument meaning, error codes and messages follow
 // the reference.  absl::uint128 -> `uint128` (unsigned __int128, same
 // layout), absl::Span -> `Span`, absl::Status(Or) -> `Status(Or)`.
-// RegisterValueType<T>() is accepted for compatibility but not required:
-// value corrections are computed generically from the ValueType.
+// Value types follow the reference's registration contract (cc:567-582,
+// 620-633): single unsigned integers are registered at construction,
+// RegisterValueType<T>() / ToValue<T>() (and the templated GenerateKeys
+// overloads, which call ToValue<T>) register T, and GenerateKeys* with a
+// Value proto of an unregistered type returns FAILED_PRECONDITION.
 #ifndef DPF_AMD_DISTRIBUTED_POINT_FUNCTION_H_
 #define DPF_AMD_DISTRIBUTED_POINT_FUNCTION_H_
 
@@ -60,15 +63,21 @@ class DistributedPointFunction {
   DistributedPointFunction(const DistributedPointFunction&) = delete;
   DistributedPointFunction& operator=(const DistributedPointFunction&) = delete;
 
+  // ToValue<T> (h:112-118): registers T, then converts.
   template <typename T>
   StatusOr<Value> ToValue(const T& in) {
+    Status status = RegisterValueType<T>();
+    if (!status.ok()) return status;
     return distributed_point_functions::ToValue(in);
   }
-  // Accepted for source compatibility; every ValueType is supported.
+  // RegisterValueType<T> (h:129-131).
   template <typename T>
   Status RegisterValueType() {
-    return OkStatus();
+    return RegisterValueTypeProto(ToValueType<T>());
   }
+  // Non-template registration by ValueType proto (the C ABI's entry).
+  Status RegisterValueTypeProto(const ValueType& value_type);
+  bool IsValueTypeRegistered(const ValueType& value_type) const;
 
   // GenerateKeys overloads (h:171-196).
   StatusOr<std::pair<DpfKey, DpfKey>> GenerateKeys(uint128 alpha, uint128 beta) {
@@ -84,7 +93,9 @@ class DistributedPointFunction {
                                         !std::is_convertible<T, Value>::value &&
                                         dpf_internal::is_supported_type<T>::value>>
   StatusOr<std::pair<DpfKey, DpfKey>> GenerateKeys(uint128 alpha, const T& beta) {
-    std::vector<Value> b{distributed_point_functions::ToValue(beta)};
+    StatusOr<Value> v = ToValue(beta);
+    if (!v.ok()) return v.status();
+    std::vector<Value> b{*v};
     return GenerateKeysIncremental(alpha, Span<const Value>(b.data(), b.size()));
   }
 
@@ -95,7 +106,11 @@ class DistributedPointFunction {
   StatusOr<std::pair<DpfKey, DpfKey>> GenerateKeysIncremental(uint128 alpha,
                                                               Span<const T> beta) {
     std::vector<Value> values;
-    for (const T& b : beta) values.push_back(distributed_point_functions::ToValue(b));
+    for (const T& b : beta) {
+      StatusOr<Value> v = ToValue(b);
+      if (!v.ok()) return v.status();
+      values.push_back(*v);
+    }
     return GenerateKeysIncremental(alpha, Span<const Value>(values.data(), values.size()));
   }
   StatusOr<std::pair<DpfKey, DpfKey>> GenerateKeysIncremental(uint128 alpha,

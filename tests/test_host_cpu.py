@@ -215,3 +215,73 @@ def test_evaluation_without_gpu_fails_loudly():
     assert e.code == 13  # INTERNAL: HIP error surfaced, no CPU fallback
     e = _err(lambda: dpf.evaluate_at(k0, 0, [1, 2]))
     assert e.code == 13
+
+
+# --- RegisterValueType (dpf/distributed_point_function.cc:567-582, 620-633;
+# distributed_point_function_test.cc:130-167) ------------------------------
+
+TUPLE_U32_NOT_REGISTERED = (
+    "No value correction function known for the following parameters:\n"
+    "log_domain_size: 10\n"
+    "value_type {\n"
+    "  tuple {\n"
+    "    elements {\n"
+    "      integer {\n"
+    "        bitsize: 32\n"
+    "      }\n"
+    "    }\n"
+    "  }\n"
+    "}\n"
+    "security_parameter: 50\n"
+    "Did you call RegisterValueType<T>() with your value type?")
+
+
+def test_keygen_fails_if_value_type_not_registered():
+    vt = V.Tuple(V.Integer(32))
+    dpf = DistributedPointFunction.create(DpfParameters(10, vt))
+    beta = vt.value_proto((42,))  # an explicit Value proto, as the reference test
+    with pytest.raises(DpfAmdError) as e:
+        dpf.generate_keys(23, beta)
+    assert e.value.code == 9  # FAILED_PRECONDITION
+    assert e.value.message.startswith("No value correction function known")
+    assert e.value.message == TUPLE_U32_NOT_REGISTERED
+    dpf.register_value_type(vt)
+    k0, k1 = dpf.generate_keys(23, beta)
+    assert k0.party == 0 and k1.party == 1
+
+
+def test_templated_keygen_registers_the_type():
+    """GenerateKeys with a typed value (ToValue<T>) registers T first."""
+    for vt, beta in ((V.Tuple(V.Integer(32), V.IntModN(64, P64)), (7, 11)),
+                     (V.XorWrapper(128), 1 << 77), (V.IntModN(32, P32), 5)):
+        dpf = DistributedPointFunction.create(DpfParameters(12, vt, 48))
+        dpf.generate_keys(99, beta)
+        dpf.generate_keys(99, vt.value_proto(beta))  # now registered
+
+
+@pytest.mark.parametrize("bits", [8, 16, 32, 64, 128])
+def test_single_integers_are_registered_at_construction(bits):
+    vt = V.Integer(bits)
+    dpf = DistributedPointFunction.create(DpfParameters(9, vt))
+    dpf.generate_keys(3, vt.value_proto(1))
+
+
+def test_unregistered_level_of_an_incremental_dpf_is_reported():
+    t = V.Tuple(V.Integer(16), V.Integer(16))
+    dpf = DistributedPointFunction.create_incremental(
+        [DpfParameters(4, V.Integer(64)), DpfParameters(8, t)])
+    with pytest.raises(DpfAmdError) as e:
+        dpf.generate_keys_incremental(5, [V.Integer(64).value_proto(1), t.value_proto((1, 2))])
+    assert e.value.code == 9
+    assert "log_domain_size: 8\n" in e.value.message
+
+
+def test_dcf_value_proto_needs_registration():
+    from distributed_point_functions_amd.dcf import DcfParameters, DistributedComparisonFunction
+    vt = V.Tuple(V.Integer(32), V.Integer(32))
+    d = DistributedComparisonFunction.create(DcfParameters(DpfParameters(8, vt)))
+    with pytest.raises(DpfAmdError) as e:
+        d.generate_keys(17, vt.value_proto((1, 2)))
+    assert e.value.code == 9
+    d.generate_keys(17, (1, 2))  # templated: registers
+    d.generate_keys(17, vt.value_proto((1, 2)))
