@@ -50,6 +50,10 @@ STATUS_NAMES = {0: "OK", 3: "INVALID_ARGUMENT", 8: "RESOURCE_EXHAUSTED",
 
 _lib = None
 
+# dpf_amd_apply_fn: int (*)(void* user, int level, const void* values, int64 n)
+APPLY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                            ctypes.c_int64)
+
 P = ctypes.c_void_p
 I64 = ctypes.c_int64
 U64 = ctypes.c_uint64
@@ -135,7 +139,7 @@ def _bind_tier2(L):
     _sig(L, "dpf_amd_evaluate_until_device", I32, P, I32, P, I64, P, SZ, P, P, I64,
          ctypes.POINTER(I64), P)
     _sig(L, "dpf_amd_evaluate_at", I32, P, P, SZ, I32, P, I64, P, SZ, P)
-    _sig(L, "dpf_amd_evaluate_and_apply", I32, P, P, P, I64, P, I32, P, SZ, P)
+    _sig(L, "dpf_amd_evaluate_and_apply", I32, P, P, P, I64, P, I32, P, SZ, P, APPLY_FN, P)
     _sig(L, "dpf_amd_dcf_create", I32, P, SZ, PP)
     _sig(L, "dpf_amd_dcf_destroy", None, P)
     _sig(L, "dpf_amd_dcf_generate_keys", I32, P, U64, U64, P, SZ, P, BUF,

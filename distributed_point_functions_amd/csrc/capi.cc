@@ -257,7 +257,8 @@ int dpf_amd_evaluate_at(const dpf_amd_dpf* dpf, const uint8_t* key, size_t key_l
 int dpf_amd_evaluate_and_apply(const dpf_amd_dpf* dpf, const uint8_t* const* keys,
                                const size_t* key_lengths, int64_t num_keys,
                                const uint64_t* points, int rightshift,
-                               const uint8_t* value_type, size_t value_type_len, void* out) {
+                               const uint8_t* value_type, size_t value_type_len, void* out,
+                               dpf_amd_apply_fn op, void* user) {
   std::vector<DpfKey> ks(num_keys);
   std::vector<const DpfKey*> ptrs(num_keys);
   for (int64_t i = 0; i < num_keys; ++i) {
@@ -272,9 +273,22 @@ int dpf_amd_evaluate_and_apply(const dpf_amd_dpf* dpf, const uint8_t* const* key
   if (!st.ok()) return Fail(st);
   std::vector<uint128> p = ToU128(points, num_keys);
   int done = 0;
+  struct Ctx {
+    dpf_amd_apply_fn op;
+    void* user;
+    const char* out;
+    int64_t n;
+    int64_t stride;
+  } ctx{op, user, static_cast<const char*>(out), num_keys,
+        dpf->dpf->value_type_descriptor(0).out_stride};
+  auto on_level = [](void* u, int h) -> bool {
+    Ctx* c = static_cast<Ctx*>(u);
+    return c->op(c->user, h, c->out + h * c->n * c->stride, c->n) != 0;
+  };
   st = dpf->dpf->EvaluateAndApplyRaw(Span<const DpfKey* const>(ptrs.data(), ptrs.size()),
                                      Span<const uint128>(p.data(), p.size()), rightshift,
-                                     dpf->dpf->value_type_descriptor(0), out, &done);
+                                     dpf->dpf->value_type_descriptor(0), out, &done,
+                                     op ? +on_level : nullptr, &ctx);
   return st.ok() ? DPF_AMD_OK : Fail(st);
 }
 

@@ -1393,7 +1393,9 @@ Status DistributedPointFunction::EvaluateAndApplyRaw(Span<const DpfKey* const> k
                                                      Span<const uint128> evaluation_points,
                                                      int rightshift,
                                                      const dpf_amd_value_type& layout,
-                                                     void* out, int* levels_done) const {
+                                                     void* out, int* levels_done,
+                                                     bool (*on_level)(void*, int),
+                                                     void* user) const {
   const DpfState& st = *state_;
   if (evaluation_points.size() != keys.size())
     return InvalidArgumentError("`keys.size()` != `evaluation_points.size()`");
@@ -1467,6 +1469,9 @@ Status DistributedPointFunction::EvaluateAndApplyRaw(Span<const DpfKey* const> k
                                   "d2h"));
     DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
     *levels_done = h + 1;
+    // h:1190-1196: stop as soon as `op` returns false (the remaining levels
+    // are never evaluated)
+    if (on_level && !on_level(user, h)) break;
   }
   return OkStatus();
 }

@@ -30,13 +30,20 @@ inline Status AbiStatus(int rc) {
   return Status(static_cast<StatusCode>(rc), dpf_amd::LastError());
 }
 
+// The calling thread's stream, destroyed when the thread exits (a server
+// answering from many short-lived threads does not accumulate streams).
 inline hipStream_t ThreadStream() {
-  thread_local hipStream_t s = [] {
-    hipStream_t x = nullptr;
-    if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) x = nullptr;
-    return x;
-  }();
-  return s;
+  struct Holder {
+    hipStream_t s = nullptr;
+    Holder() {
+      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+    }
+    ~Holder() {
+      if (s) hipStreamDestroy(s);
+    }
+  };
+  thread_local Holder h;
+  return h.s;
 }
 
 // Host-side phase timer: with DPF_AMD_TRACE_HOST set, Mark(name) prints the

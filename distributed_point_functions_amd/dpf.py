@@ -318,10 +318,20 @@ class DistributedPointFunction:
         pw = u128_words(_seq(points)) if len(points) else np.zeros(2, np.uint64)
         H = len(self.parameters)
         out = np.zeros(max(H * len(keys), 1), dtype=vt.numpy_dtype())
+        n = len(keys)
+        errors = []
+
+        def on_level(user, h, values, num):
+            # called by the library after level h is evaluated; 0 stops the
+            # remaining levels (h:1190-1196)
+            try:
+                return 1 if op(vt.decode(out[h * n:(h + 1) * n])) else 0
+            except Exception as e:  # pragma: no cover - surfaced below
+                errors.append(e)
+                return 0
+        cb = _lib.APPLY_FN(on_level)
         check(_lib.lib().dpf_amd_evaluate_and_apply(
             self._h, arr, lens, len(keys), pw.ctypes.data_as(ctypes.c_void_p), rightshift,
-            tp, len(tp), out.ctypes.data_as(ctypes.c_void_p)))
-        n = len(keys)
-        for h in range(H):
-            if not op(vt.decode(out[h * n:(h + 1) * n])):
-                break
+            tp, len(tp), out.ctypes.data_as(ctypes.c_void_p), cb, None))
+        if errors:
+            raise errors[0]

@@ -100,12 +100,30 @@ class DenseDpfPirDatabase:
     def max_value_size(self) -> int:
         return _lib.lib().dpf_amd_pir_db_max_value_size(self._h)
 
+    @property
+    def record_stride(self) -> int:
+        """Device row stride in bytes of the built database (0 before build)."""
+        stride = ctypes.c_int64(0)
+        _lib.lib().dpf_amd_pir_db_device_records(self._h, ctypes.byref(stride))
+        return stride.value
+
     def inner_product_with(self, selections: Sequence[Sequence[int]]) -> List[bytes]:
         """InnerProductWith (pir/pir_database_interface.h:65-66)."""
         q = len(selections)
         if q == 0:
             return []
         nb = len(selections[0])
+        # pir_internal::InnerProduct's checks (inner_product_hwy.cc:306-323),
+        # before the flat buffer of q * nb blocks crosses the C ABI
+        for i, s_i in enumerate(selections):
+            if len(s_i) * BITS_PER_BLOCK < self.size:
+                raise _lib.DpfAmdError(3, "`selections[%d]` contains insufficient number of "
+                                          "bits: %d, expected: %d"
+                                       % (i, len(s_i) * BITS_PER_BLOCK, self.size))
+            if len(s_i) != nb:
+                raise _lib.DpfAmdError(3, "`selections[%d].size()` does not match "
+                                          "`selections[0].size()`: actual%d, expected %d"
+                                       % (i, len(s_i), nb))
         sel = u128_words([b for s in selections for b in s])
         out = np.zeros(max(1, q * self.max_value_size), dtype=np.uint8)
         check(_lib.lib().dpf_amd_pir_db_inner_product(

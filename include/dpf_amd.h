@@ -311,15 +311,20 @@ int dpf_amd_evaluate_at(const dpf_amd_dpf* dpf, const uint8_t* key,
                         const uint8_t* value_type, size_t value_type_len,
                         void* out);
 
-/* EvaluateAndApply<T, Fn> (h:403-407, 1072-1198) without the callback:
- * evaluates key i at point i for every hierarchy level and writes
- * num_levels * num_keys host-layout T values (level-major) to `out`. */
+/* EvaluateAndApply<T, Fn> (h:403-407, 1072-1198): evaluates key i at point
+ * i level by level, writing num_keys host-layout T values of level h to
+ * out + h * num_keys * sizeof(T); after each level `op(user, h, values of
+ * level h, num_keys)` is called (if not NULL) and a return of 0 stops the
+ * evaluation, as the reference's `op` returning false. */
+typedef int (*dpf_amd_apply_fn)(void* user, int hierarchy_level, const void* values,
+                                int64_t num_keys);
 int dpf_amd_evaluate_and_apply(const dpf_amd_dpf* dpf,
                                const uint8_t* const* keys,
                                const size_t* key_lengths, int64_t num_keys,
                                const uint64_t* points, int rightshift,
                                const uint8_t* value_type,
-                               size_t value_type_len, void* out);
+                               size_t value_type_len, void* out,
+                               dpf_amd_apply_fn op, void* user);
 
 /* DistributedComparisonFunction (dcf/distributed_comparison_function.h:30-
  * 187).  Parameters and keys cross as DcfParameters / DcfKey protos; beta as

@@ -181,14 +181,19 @@ class DistributedPointFunction {
     const int levels = num_hierarchy_levels();
     std::vector<T> values(keys.size() * static_cast<size_t>(levels));
     int done = 0;
-    DPF_RETURN_IF_ERROR(EvaluateAndApplyRaw(keys, evaluation_points,
-                                            evaluation_points_rightshift, LayoutOf<T>(),
-                                            values.data(), &done));
-    for (int h = 0; h < levels; ++h) {
-      Span<const T> level(values.data() + h * keys.size(), keys.size());
-      if (!op(level)) break;
-    }
-    return OkStatus();
+    // op runs after each level is evaluated; a false return stops the
+    // evaluation of the remaining levels (h:1190-1196)
+    struct Ctx {
+      Fn* op;
+      const T* values;
+      size_t n;
+    } ctx{&op, values.data(), keys.size()};
+    auto on_level = [](void* user, int h) -> bool {
+      Ctx* c = static_cast<Ctx*>(user);
+      return (*c->op)(Span<const T>(c->values + h * c->n, c->n));
+    };
+    return EvaluateAndApplyRaw(keys, evaluation_points, evaluation_points_rightshift,
+                               LayoutOf<T>(), values.data(), &done, on_level, &ctx);
   }
 
   Span<const DpfParameters> parameters() const;
@@ -210,9 +215,13 @@ class DistributedPointFunction {
   Status EvaluateAtRaw(const DpfKey& key, int hierarchy_level,
                        Span<const uint128> evaluation_points, EvaluationContext* ctx,
                        const dpf_amd_value_type& vt, void* out) const;
+  // After each level's values are in `out`, `on_level(user, level)` (if
+  // set) decides whether to continue.
   Status EvaluateAndApplyRaw(Span<const DpfKey* const> keys,
                              Span<const uint128> evaluation_points, int rightshift,
-                             const dpf_amd_value_type& vt, void* out, int* levels_done) const;
+                             const dpf_amd_value_type& vt, void* out, int* levels_done,
+                             bool (*on_level)(void*, int) = nullptr,
+                             void* user = nullptr) const;
   // ProtoValidator::ValidateDpfKey (proto_validator.cc:205-236).
   Status ValidateKey(const DpfKey& key) const;
   // The value correction of `key` at hierarchy `level` as flattened 128-bit

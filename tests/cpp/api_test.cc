@@ -131,8 +131,67 @@ static int DcfGenEval() {
   return 0;
 }
 
+// KeyGenerationFailsIfValueTypeNotRegistered (distributed_point_function_
+// test.cc:148-167) and the templated overload registering T (:130-146).
+static int Registration() {
+  DpfParameters p;
+  p.set_log_domain_size(10);
+  p.mutable_value_type()->mutable_tuple()->add_elements()->mutable_integer()->set_bitsize(32);
+  auto dpf = DistributedPointFunction::Create(p);
+  CHECK_OK(dpf);
+  Value beta;
+  beta.mutable_tuple()->add_elements()->mutable_integer()->set_value_uint64(42);
+  auto bad = (*dpf)->GenerateKeys(23, beta);
+  CHECK(!bad.ok() && bad.status().code() == StatusCode::kFailedPrecondition);
+  CHECK(!bad.ok() && bad.status().message().rfind("No value correction function known", 0) == 0);
+  auto good = (*dpf)->GenerateKeys(23, Tuple<uint32_t>(42u));  // ToValue<T> registers T
+  CHECK_OK(good);
+  auto again = (*dpf)->GenerateKeys(23, beta);
+  CHECK_OK(again);
+  return 0;
+}
+
+// EvaluateAndApply stops evaluating when op returns false (h:1190-1196).
+static int EvaluateAndApplyStops() {
+  std::vector<DpfParameters> ps(3);
+  for (int h = 0; h < 3; ++h) {
+    ps[h].set_log_domain_size(8 * (h + 1));
+    ps[h].mutable_value_type()->mutable_integer()->set_bitsize(64);
+  }
+  auto dpf = DistributedPointFunction::CreateIncremental(ps);
+  CHECK_OK(dpf);
+  auto keys = (*dpf)->GenerateKeysIncremental(uint128{0x123456},
+                                              std::vector<uint128>{1, 2, 3});
+  CHECK_OK(keys);
+  std::vector<DpfKey> ks = {keys->first, keys->second};
+  std::vector<uint128> pts = {0x123456, 0x123456};
+  int calls = 0;
+  auto st = (*dpf)->EvaluateAndApply<uint64_t>(
+      Span<const DpfKey>(ks.data(), ks.size()), Span<const uint128>(pts.data(), pts.size()),
+      [&calls](Span<const uint64_t> v) {
+        ++calls;
+        return v.size() == 2 && calls < 2;  // stop after the second level
+      });
+  CHECK(st.ok());
+  CHECK(calls == 2);
+  int all = 0;
+  std::vector<uint64_t> sums;
+  st = (*dpf)->EvaluateAndApply<uint64_t>(
+      Span<const DpfKey>(ks.data(), ks.size()), Span<const uint128>(pts.data(), pts.size()),
+      [&](Span<const uint64_t> v) {
+        ++all;
+        sums.push_back(v[0] + v[1]);
+        return true;
+      });
+  CHECK(st.ok() && all == 3);
+  CHECK(sums == std::vector<uint64_t>({1, 2, 3}));
+  return 0;
+}
+
 int main() {
-  if (FullDomainUint64() || IncrementalTuple() || DcfGenEval()) return 2;
+  if (FullDomainUint64() || IncrementalTuple() || DcfGenEval() || Registration() ||
+      EvaluateAndApplyStops())
+    return 2;
   if (failures) {
     std::fprintf(stderr, "%d check(s) failed\n", failures);
     return 1;

@@ -197,6 +197,34 @@ def test_pir_database_inner_product_vs_oracle(api, n, size):
     assert db.inner_product_with(sels) == po.inner_product(records, sels)
 
 
+@pytest.mark.parametrize("size,default,padded", [(16, 16, 32), (64, 64, 64), (240, 256, 256),
+                                                 (1040, 1040, 2048), (100, 128, 128), (200, 208, 256)])
+def test_pir_database_stride_choice_and_forced_strides(api, monkeypatch, size, default, padded):
+    """Builder's device stride (pir.cc ChooseStride): padded to a KPirScanG
+    width only within 25 % and an HBM budget; DPF_AMD_PIR_STRIDE forces either
+    layout, and every layout answers as the oracle."""
+    _, _, P = api
+    n = 3001
+    records = _records(n, size, size)
+    arr = np.frombuffer(b"".join(records), np.uint8).reshape(n, size)
+    rng = random.Random(size)
+    sels = [[rng.getrandbits(128) for _ in range((n + 127) // 128)] for _ in range(20)]
+    want = po.inner_product(records, sels)
+    aligned = (size + 15) // 16 * 16
+    for force, stride in ((None, default), ("aligned", aligned), ("padded", padded)):
+        if force:
+            monkeypatch.setenv("DPF_AMD_PIR_STRIDE", force)
+        else:
+            monkeypatch.delenv("DPF_AMD_PIR_STRIDE", raising=False)
+        db = P.DenseDpfPirDatabase()
+        db.insert_fixed(arr)
+        db.build()
+        assert db.record_stride == stride, force
+        assert db.max_value_size == size
+        assert db.inner_product_with(sels) == want, force
+        assert db.inner_product_with(sels[:1]) == want[:1], force
+
+
 def _pir_setup(api, n, size, seed=0):
     D, V, P = api
     records = _records(n, size, seed)

@@ -1,0 +1,76 @@
+"""Concurrency of the const API under 1024 threads, as the reference's stress
+tests: one Aes128FixedKeyHash shared by 1024 threads
+(dpf/aes_128_fixed_key_hash_test.cc:155-174) and one DenseDpfPirServer
+answering the same request from 1024 threads
+(pir/dense_dpf_pir_server_test.cc:307-326).  Here the shared objects are a
+DistributedPointFunction (EvaluateAt, full-domain EvaluateNext with one
+context per thread) and a DenseDpfPirServer; every thread's result must equal
+the single-threaded one.  ctypes releases the GIL during the library calls,
+so the threads really run the host paths and kernels concurrently (each on
+its own HIP stream).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+THREADS = 1024
+
+
+def _run_threads(fn):
+    results, errors = [None] * THREADS, []
+
+    def worker(t):
+        try:
+            results[t] = fn(t)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(THREADS)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    assert not errors, errors[:3]
+    return results
+
+
+def test_dpf_evaluate_concurrently_from_1024_threads(cuda):
+    from distributed_point_functions_amd import value_types as V
+    from distributed_point_functions_amd.dpf import DistributedPointFunction, DpfParameters
+    vt = V.Tuple(V.Integer(32), V.IntModN(64, 2 ** 64 - 59))
+    dpf = DistributedPointFunction.create(DpfParameters(12, vt, 48))
+    k0, _ = dpf.generate_keys(1234, (5, 6), seeds=(11, 12))
+    pts = [(17 * i + 3) % 4096 for i in range(64)] + [1234]
+    want_at = dpf.evaluate_at(k0, 0, pts, raw=True).tobytes()
+    want_full = dpf.evaluate_next([], dpf.create_evaluation_context(k0), raw=True).tobytes()
+
+    def call(t):
+        if t % 2:
+            return dpf.evaluate_at(k0, 0, pts, raw=True).tobytes() == want_at
+        ctx = dpf.create_evaluation_context(k0)
+        return dpf.evaluate_next([], ctx, raw=True).tobytes() == want_full
+    assert all(_run_threads(call))
+
+
+def test_pir_server_handle_request_from_1024_threads(cuda):
+    from distributed_point_functions_amd import pir as P
+    from distributed_point_functions_amd import value_types as V
+    from distributed_point_functions_amd.dpf import DistributedPointFunction, DpfParameters
+    n, size = 2000, 64
+    rng = np.random.default_rng(1024)
+    records = rng.integers(0, 256, (n, size), dtype=np.uint8)
+    db = P.DenseDpfPirDatabase()
+    db.insert_fixed(records)
+    server = P.DenseDpfPirServer.create_plain(n, db)
+    dpf = DistributedPointFunction.create(DpfParameters((n - 1).bit_length(), V.XorWrapper(128)))
+    idx = [0, 77, 1999, 1024]
+    pairs = P.client_keys(dpf, n, idx, seeds=[(2 * i + 5, 2 * i + 6) for i in range(len(idx))])
+    req0 = P.pir_request_plain([a for a, _ in pairs])
+    req1 = P.pir_request_plain([b for _, b in pairs])
+    want0 = server.handle_request(req0)
+    r1 = P.parse_response(server.handle_request(req1))
+    for i, a, b in zip(idx, P.parse_response(want0), r1):
+        assert bytes(x ^ y for x, y in zip(a, b)) == records[i].tobytes()
+    assert all(_run_threads(lambda t: server.handle_request(req0) == want0))
