@@ -203,3 +203,58 @@ def test_oracle_reproduces_golden_inner_product(golden):
                 for j, b in enumerate(r):
                     acc[j] ^= b
         assert bytes(acc).hex() == g["out_hex"][q]
+
+
+# ------------------------------------------------ AES-128-CTR seeded PRNG
+# Aes128CtrSeededPrng (pir/prng/aes_128_ctr_seeded_prng.cc:60-101): key =
+# seed, all-zero IV, AES_ctr128_encrypt of zeros (big-endian 128-bit counter).
+CTR_FIXED_SEED_KAT = bytes.fromhex(
+    "c6a13b37878f5b826f4f8162a1c8d879734613 9595c0b41e497bbde365f42d0a".replace(" ", ""))
+
+
+def test_aes_ctr_prng_fixed_seed_known_answer():
+    """aes_128_ctr_seeded_prng_test.cc:129-148."""
+    assert po.aes_ctr_prng(bytes(range(16)), 32) == CTR_FIXED_SEED_KAT
+    assert po.aes_ctr_prng(bytes(range(16)), 0) == b""
+
+
+def _evp_aes_128_ctr(key: bytes, iv: bytes, chunks):
+    """libcrypto EVP_aes_128_ctr over zero bytes, one EncryptUpdate per chunk."""
+    import ctypes
+    import ctypes.util
+    name = ctypes.util.find_library("crypto")
+    if not name:
+        pytest.skip("libcrypto not present")
+    L = ctypes.CDLL(name)
+    L.EVP_CIPHER_CTX_new.restype = ctypes.c_void_p
+    L.EVP_aes_128_ctr.restype = ctypes.c_void_p
+    L.EVP_EncryptInit_ex.argtypes = [ctypes.c_void_p] * 5
+    L.EVP_EncryptUpdate.argtypes = [ctypes.c_void_p, ctypes.c_char_p,
+                                    ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_int]
+    L.EVP_CIPHER_CTX_free.argtypes = [ctypes.c_void_p]
+    ctx = L.EVP_CIPHER_CTX_new()
+    try:
+        assert L.EVP_EncryptInit_ex(ctx, L.EVP_aes_128_ctr(), None, key, iv) == 1
+        out = b""
+        for n in chunks:
+            buf = ctypes.create_string_buffer(max(n, 1))
+            outl = ctypes.c_int(0)
+            assert L.EVP_EncryptUpdate(ctx, buf, ctypes.byref(outl), bytes(n), n) == 1
+            out += buf.raw[:outl.value]
+        return out
+    finally:
+        L.EVP_CIPHER_CTX_free(ctx)
+
+
+@pytest.mark.parametrize("seed_hex,length", [
+    ("000102030405060708090a0b0c0d0e0f", 32),
+    ("ffffffffffffffffffffffffffffffff", 1000),
+    ("0123456789abcdeffedcba9876543210", 4099),
+    ("8899aabbccddeeff0011223344556677", 1 << 16),
+])
+def test_aes_ctr_prng_matches_libcrypto(seed_hex, length):
+    seed = bytes.fromhex(seed_hex)
+    want = _evp_aes_128_ctr(seed, bytes(16), [length])
+    assert po.aes_ctr_prng(seed, length) == want
+    # GetRandomBytes in pieces continues the same stream (test.cc:81-91)
+    assert _evp_aes_128_ctr(seed, bytes(16), [7, 0, 16, 1, length - 24]) == want
