@@ -192,20 +192,31 @@ def bench_pir(args, world, rank, device):
                 records=n)
 
 
+def library_sha256():
+    import hashlib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def traffic_from_profiles(kernel_substr):
-    """HBM bytes per launch of a kernel from the newest committed PMC summary
-    (profiles/<round>_pmc.json, written by tools/summarize_profile.py from
-    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench)."""
+    """(HBM bytes per launch, profile file) of a kernel from a committed PMC
+    summary of THIS build (profiles/<round>_pmc.json, written by
+    tools/summarize_profile.py from separate rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of this bench, keyed by the profiled library's
+    sha256); (None, None) when no summary matches the loaded library."""
     import glob
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                          "profiles", "r*_pmc.json")))
+                                          "profiles", "r*_pmc.json")), key=os.path.getmtime)
+    sha = library_sha256()
     for f in reversed(files):
         with open(f) as fh:
             d = json.load(fh)
+        if d.get("_meta", {}).get("library_sha256") != sha:
+            continue
         for name, e in d.items():
             if kernel_substr in name and "hbm_bytes" in e:
-                return e["hbm_bytes"]
-    return None
+                return e["hbm_bytes"], os.path.basename(f)
+    return None, None
 
 
 def _cpu_worker(job):
@@ -282,11 +293,13 @@ def main():
         aes_s = aes_per_launch / (r["kernel_ms"] / 1e3)
         achieved = aes_s * OPS_PER_AES / 1e12
         lookups_s = LDS_LOOKUPS_PER_LEAF_C5 * (leaves / world) / (r["kernel_ms"] / 1e3)
+        expand_traffic = traffic_from_profiles("KExpand<8, dpf_amd::EmitU32ModN64>")
+        scan_traffic = traffic_from_profiles("KPirScanG<1, 4>")
         out = {
             "metric": METRIC, "value": value, "unit": "leaves/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-            "dtype": "u32", "data": "synthetic (fixed-seed DPF key)",
+            "dtype": "tuple<u32,intmodn<u64>>", "data": "synthetic (fixed-seed DPF key)",
             "config": {"workload": "c5: full-domain EvaluateNext, log_domain_size=%d, "
                                    "Tuple<uint32,IntModN<uint64,2^64-59>>, "
                                    "security_parameter=48" % args.log_domain,
@@ -301,8 +314,9 @@ def main():
                          "achieved": lookups_s / 1e12,
                          "peak": LDS_PEAK_LOOKUPS / 1e12, "unit": "T lookups/s",
                          "frac": lookups_s / LDS_PEAK_LOOKUPS,
-                         "traffic": traffic_from_profiles("KExpand<8, dpf_amd::EmitU32ModN64>"),
-                         "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/)",
+                         "traffic": expand_traffic[0],
+                         "traffic_unit": "HBM bytes per launch (rocprofv3 PMC of this build)",
+                         "traffic_profile": expand_traffic[1],
                          "algorithmic_bytes": leaves // world * 16,
                          "kernel": "KExpand<8,EmitU32ModN64>", "kernel_ms": r["kernel_ms"],
                          "aes_per_launch": aes_per_launch, "aes_per_leaf": AES_PER_LEAF_C5,
@@ -328,7 +342,7 @@ def main():
                 "scaling": "strong",
                 "roofline": {"bound": "hbm", "achieved": scan_gbs, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": scan_gbs / HBM_PEAK_GBS,
-                             "traffic": traffic_from_profiles("KPirScanG<1, 4>"),
+                             "traffic": scan_traffic[0], "traffic_profile": scan_traffic[1],
                              "algorithmic_bytes": pir["per_gpu_bytes"],
                              "kernel": "KPirScanG<1,4>+KXorFold", "kernel_ms": pir["scan_ms"]},
             }

@@ -20,6 +20,9 @@ LIB = os.path.join(OUT_DIR, "libdpf_amd.so")
 # C++ API consumer test (tests/cpp/api_test.cc) linked against LIB.
 CPP_TEST_SRC = os.path.join(ROOT, "tests", "cpp", "api_test.cc")
 CPP_TEST = os.path.join(OUT_DIR, "cpp_api_test")
+# C++ API wall-clock bench of the BASELINE configs c1-c3 (tools/cpp_api_bench.cc).
+CPP_BENCH_SRC = os.path.join(ROOT, "tools", "cpp_api_bench.cc")
+CPP_BENCH = os.path.join(OUT_DIR, "cpp_api_bench")
 ARCH = os.environ.get("DPF_AMD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -68,17 +71,18 @@ def build(force: bool = False, jobs: int = 8) -> str:
         subprocess.check_call(["hipcc", "--offload-arch=" + ARCH, "-shared", "-fPIC",
                                "-o", tmp] + objs + ["-lpthread"])
         os.replace(tmp, LIB)
-    if os.path.exists(CPP_TEST_SRC) and (
-            force or not os.path.exists(CPP_TEST) or
-            os.path.getmtime(CPP_TEST) < max(os.path.getmtime(LIB),
-                                             os.path.getmtime(CPP_TEST_SRC), _headers_mtime())):
-        # the reference's C++ API, compiled as a caller would: plain g++ on
-        # include/ and the shared library, no HIP toolchain
-        tmp = CPP_TEST + ".tmp%d" % os.getpid()
-        subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall",
-                               "-I" + os.path.join(ROOT, "include"), CPP_TEST_SRC,
-                               "-L" + OUT_DIR, "-ldpf_amd", "-Wl,-rpath,$ORIGIN", "-o", tmp])
-        os.replace(tmp, CPP_TEST)
+    for src, exe in ((CPP_TEST_SRC, CPP_TEST), (CPP_BENCH_SRC, CPP_BENCH)):
+        if os.path.exists(src) and (
+                force or not os.path.exists(exe) or
+                os.path.getmtime(exe) < max(os.path.getmtime(LIB), os.path.getmtime(src),
+                                            _headers_mtime())):
+            # the reference's C++ API, compiled as a caller would: plain g++ on
+            # include/ and the shared library, no HIP toolchain
+            tmp = exe + ".tmp%d" % os.getpid()
+            subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall",
+                                   "-I" + os.path.join(ROOT, "include"), src,
+                                   "-L" + OUT_DIR, "-ldpf_amd", "-Wl,-rpath,$ORIGIN", "-o", tmp])
+            os.replace(tmp, exe)
     return LIB
 
 

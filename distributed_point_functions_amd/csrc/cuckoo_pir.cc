@@ -487,10 +487,10 @@ StatusOr<PirResponse> CuckooHashingSparseDpfPirServer::HandlePlainRequest(
     void* sel = nullptr;
     DPF_RETURN_IF_ERROR(HipStatus(hipMallocAsync(&sel, 16 * blocks * q, s), "alloc"));
     const dpf_amd_value_type layout = dpf_internal::HostLayoutOf<XorWrapper<uint128>>();
-    Status st;
-    for (int i = 0; i < q && st.ok(); ++i)
-      st = dpf_->ExpandLeavesOnDevice(plain.dpf_key(i), 0, blocks, layout,
-                                      static_cast<char*>(sel) + 16 * blocks * i, s);
+    std::vector<const DpfKey*> keys(q);
+    for (int i = 0; i < q; ++i) keys[i] = &plain.dpf_key(i);
+    Status st = dpf_->ExpandLeavesOnDeviceBatched(
+        Span<const DpfKey* const>(keys.data(), keys.size()), blocks, layout, sel, s);
     StatusOr<std::vector<Database::RecordType>> r =
         st.ok() ? gpu_db->InnerProductWithDevice(sel, blocks, q, s)
                 : StatusOr<std::vector<Database::RecordType>>(st);

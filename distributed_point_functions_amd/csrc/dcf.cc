@@ -15,6 +15,7 @@
 namespace distributed_point_functions {
 
 using dpf_internal_host::AbiStatus;
+using dpf_internal_host::ClearPadding;
 using dpf_internal_host::DeviceBuffer;
 using dpf_internal_host::HipStatus;
 using dpf_internal_host::ThreadStream;
@@ -162,6 +163,7 @@ Status DistributedComparisonFunction::BatchEvaluateRaw(Span<const DcfKey* const>
   DPF_RETURN_IF_ERROR(dccr.Upload(ccr.data(), ccr.size(), s));
   DPF_RETURN_IF_ERROR(dcorr.Upload(corr.data(), 16 * corr.size(), s));
   DPF_RETURN_IF_ERROR(dout.Alloc(n * vt.out_stride, s));
+  DPF_RETURN_IF_ERROR(ClearPadding(vt, dout.get(), n * vt.out_stride, s));
   DPF_RETURN_IF_ERROR(
       HipStatus(hipMemsetAsync(dout.get(), 0, n * vt.out_stride, s), "memset"));
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_dcf_evaluate(

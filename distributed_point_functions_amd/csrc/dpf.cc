@@ -716,6 +716,7 @@ bool DistributedPointFunction::IsValueTypeRegistered(const ValueType& value_type
 // Device helpers: csrc/host_device.h
 // ---------------------------------------------------------------------------
 using dpf_internal_host::AbiStatus;
+using dpf_internal_host::ClearPadding;
 using dpf_internal_host::DeviceBuffer;
 using dpf_internal_host::HipStatus;
 using dpf_internal_host::HostTrace;
@@ -1286,6 +1287,7 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
     DPF_RETURN_IF_ERROR(staging.Alloc(expanded * stride, s));
     expand_out = staging.get();
   }
+  DPF_RETURN_IF_ERROR(ClearPadding(vt, expand_out, expanded * stride, s));
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_expand_and_correct(
       num_roots, root_seeds.get(), root_cb.as<uint8_t>(), levels, cws.get(), ccl.as<uint8_t>(),
       ccr.as<uint8_t>(), &vt, reinterpret_cast<const uint64_t*>(corr.data()),
@@ -1378,6 +1380,7 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
   DPF_RETURN_IF_ERROR(ccl.Upload(cw.ccl.data(), levels, s));
   DPF_RETURN_IF_ERROR(ccr.Upload(cw.ccr.data(), levels, s));
   DPF_RETURN_IF_ERROR(dout.Alloc(n * vt.out_stride, s));
+  DPF_RETURN_IF_ERROR(ClearPadding(vt, dout.get(), n * vt.out_stride, s));
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_points(
       n, seeds.get(), cbs.as<uint8_t>(), paths.get(), 0, levels, levels, cws.get(),
       ccl.as<uint8_t>(), ccr.as<uint8_t>(), &vt, bi.as<uint8_t>(), nullptr, key.party(), nullptr,
@@ -1459,6 +1462,7 @@ Status DistributedPointFunction::EvaluateAndApplyRaw(Span<const DpfKey* const> k
     DPF_RETURN_IF_ERROR(dcorr.Upload(corr.data(), 16 * corr.size(), s));
     DPF_RETURN_IF_ERROR(dbi.Upload(bidx.data(), n, s));
     DPF_RETURN_IF_ERROR(dout.Alloc(n * vt.out_stride, s));
+    DPF_RETURN_IF_ERROR(ClearPadding(vt, dout.get(), n * vt.out_stride, s));
     DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_points(
         n, seeds.get(), cbs.as<uint8_t>(), paths.get(), std::min(tree_rs, 255), levels,
         static_cast<int64_t>(levels) * n, dcws.get(), dccl.as<uint8_t>(), dccr.as<uint8_t>(),
@@ -1504,6 +1508,73 @@ Status DistributedPointFunction::ExpandLeavesOnDevice(const DpfKey& key, int64_t
       1, rs.get(), rc.as<uint8_t>(), m.tree_level, cws.get(), ccl.as<uint8_t>(),
       ccr.as<uint8_t>(), &vt, reinterpret_cast<const uint64_t*>(corr.data()), key.party(), cepb,
       leaf_begin, leaf_end, out, s));
+}
+
+
+Status DistributedPointFunction::ExpandLeavesOnDeviceBatched(Span<const DpfKey* const> keys,
+                                                             int64_t num_leaves,
+                                                             const dpf_amd_value_type& layout,
+                                                             void* out, void* stream) const {
+  const DpfState& st = *state_;
+  const int64_t q = static_cast<int64_t>(keys.size());
+  if (q == 0 || num_leaves <= 0) return OkStatus();
+  for (const DpfKey* k : keys) DPF_RETURN_IF_ERROR(ValidateDpfKey(st, *k));
+  const int h = num_hierarchy_levels() - 1;
+  const LevelMeta& m = st.levels[h];
+  if (m.tree_level > 62) return InvalidArgumentError("domain too large to expand fully");
+  if (num_leaves > (int64_t{1} << m.tree_level))
+    return InvalidArgumentError("leaf range out of bounds");
+  dpf_amd_value_type vt;
+  DPF_RETURN_IF_ERROR(MergeLayout(m, layout, &vt));
+  const int L = m.tree_level;
+  const int cepb = 1 << (m.log_domain - L);
+  // A per-leaf walk costs L + 1 AES against ~2 for the tree expansion, but
+  // the whole batch is one upload and one launch: the better trade while the
+  // batch is a few million AES (cuckoo-table selections, small databases).
+  const bool walk = q > 1 && cepb == 1 &&
+                    static_cast<double>(q) * num_leaves * (L + 1) <= static_cast<double>(1 << 25);
+  char* o = static_cast<char*>(out);
+  if (!walk) {
+    for (int64_t i = 0; i < q; ++i)
+      DPF_RETURN_IF_ERROR(ExpandLeavesOnDevice(*keys[i], 0, num_leaves, layout,
+                                               o + i * num_leaves * cepb * vt.out_stride, stream));
+    return OkStatus();
+  }
+  std::vector<uint128> corr;
+  DPF_RETURN_IF_ERROR(CorrectionsFor(st, *keys[0], h, &corr));
+  const int64_t per = static_cast<int64_t>(corr.size());
+  // One host image of every key's inputs: seeds [q] | correction seeds
+  // [q][L] | value corrections [q][per] (16-byte words), then control bits
+  // [q], parties [q], ccl [q][L], ccr [q][L].
+  const int64_t off_cw = 16 * q, off_corr = off_cw + 16 * q * L;
+  const int64_t off_cb = off_corr + 16 * q * per, off_party = off_cb + q;
+  const int64_t off_ccl = off_party + q, off_ccr = off_ccl + q * L;
+  std::vector<char> host(off_ccr + q * L + 16, 0);
+  for (int64_t k = 0; k < q; ++k) {
+    const DpfKey& key = *keys[k];
+    const uint128 seed = MakeUint128(key.seed().high(), key.seed().low());
+    memcpy(host.data() + 16 * k, &seed, 16);
+    const CwArrays cw = KeyCws(key, 0, L);
+    if (L > 0) {
+      memcpy(host.data() + off_cw + 16 * k * L, cw.seeds.data(), 16 * L);
+      memcpy(host.data() + off_ccl + k * L, cw.ccl.data(), L);
+      memcpy(host.data() + off_ccr + k * L, cw.ccr.data(), L);
+    }
+    if (k > 0) DPF_RETURN_IF_ERROR(CorrectionsFor(st, key, h, &corr));
+    if (static_cast<int64_t>(corr.size()) != per) return InternalError("correction size mismatch");
+    memcpy(host.data() + off_corr + 16 * k * per, corr.data(), 16 * per);
+    host[off_cb + k] = static_cast<char>(key.party() != 0);
+    host[off_party + k] = static_cast<char>(key.party());
+  }
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ThreadStream();
+  DeviceBuffer dev;
+  DPF_RETURN_IF_ERROR(dev.Upload(host.data(), host.size(), s));
+  char* d = dev.as<char>();
+  return AbiStatus(dpf_amd_evaluate_points_batched(
+      q, num_leaves, d, reinterpret_cast<const uint8_t*>(d + off_cb), nullptr, 0, L, d + off_cw,
+      reinterpret_cast<const uint8_t*>(d + off_ccl), reinterpret_cast<const uint8_t*>(d + off_ccr),
+      &vt, nullptr, reinterpret_cast<const int8_t*>(d + off_party), 0, d + off_corr, nullptr, out,
+      s));
 }
 
 }  // namespace distributed_point_functions

@@ -68,6 +68,20 @@ class HostTrace {
   std::chrono::steady_clock::time_point t_;
 };
 
+// Host layouts with holes (e.g. {uint32_t, uint64_t}: 16 bytes, 4 unused):
+// the kernels write only the scalars, so a buffer whose rows reach the caller
+// is cleared first and stale device memory never shows up in the padding.
+inline bool HasPadding(const dpf_amd_value_type& vt) {
+  int used = 0;
+  for (int i = 0; i < vt.num_scalars; ++i) used += vt.scalars[i].bytes;
+  return used < vt.out_stride;
+}
+
+inline Status ClearPadding(const dpf_amd_value_type& vt, void* p, size_t bytes, hipStream_t s) {
+  if (bytes == 0 || !HasPadding(vt)) return OkStatus();
+  return HipStatus(hipMemsetAsync(p, 0, bytes, s), "hipMemsetAsync");
+}
+
 class DeviceBuffer {
  public:
   DeviceBuffer() = default;

@@ -154,7 +154,10 @@ __device__ __forceinline__ void FoldPartials(const ScanArgs& a, const uint4 (&ac
     __syncthreads();
     if (threadIdx.x < Cs) {
       uint4 r = make_uint4(0, 0, 0, 0);
+      // rolled: an unrolled G = 64 fold alone needs 256 VGPRs
+#pragma unroll 1
       for (int w = 0; w < kScanWaves; ++w)
+#pragma unroll 4
         for (int g = 0; g < G; ++g) {
           uint4 x = red[w * 64 + g * Cs + threadIdx.x];
           r.x ^= x.x;
@@ -168,74 +171,28 @@ __device__ __forceinline__ void FoldPartials(const ScanArgs& a, const uint4 (&ac
   }
 }
 
-template <int QN>
-__global__ __launch_bounds__(kScanBlock) void KPirScan(ScanArgs a) {
-  __shared__ uint4 red[kScanBlock];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int chunk_lo = blockIdx.y * 64;
-  const int Cs = min(64, a.C - chunk_lo);
-  const int G = 64 / Cs;
-  const bool active = lane < G * Cs;
-  const int my_chunk = chunk_lo + (lane % Cs);
-  const int my_rec = lane / Cs;
-  uint4 acc[QN];
-#pragma unroll
-  for (int q = 0; q < QN; ++q) acc[q] = make_uint4(0, 0, 0, 0);
-
-  const int64_t tiles = (a.num_records + 127) >> 7;
-  const int64_t wstride = (int64_t)gridDim.x * kScanWaves;
-  for (int64_t tile = (int64_t)blockIdx.x * kScanWaves + wave; tile < tiles; tile += wstride) {
-    uint4 sw[QN];
-#pragma unroll
-    for (int q = 0; q < QN; ++q)
-      sw[q] = (q < a.nq) ? a.sel[(int64_t)(a.q0 + q) * a.sel_blocks + tile]
-                         : make_uint4(0, 0, 0, 0);
-    const int64_t rec0 = tile << 7;
-    for (int it = 0; it < 128; it += G * kScanUnroll) {
-      uint4 v[kScanUnroll];
-      int rr[kScanUnroll];
-#pragma unroll
-      for (int u = 0; u < kScanUnroll; ++u) {
-        rr[u] = it + u * G + my_rec;
-        const int64_t rec = rec0 + rr[u];
-        const bool ok = active && rr[u] < 128 && rec < a.num_records;
-        v[u] = ok ? LoadRecordWord(&a.db[rec * a.C + my_chunk]) : make_uint4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int u = 0; u < kScanUnroll; ++u) {
-        const int r = rr[u] & 127;
-#pragma unroll
-        for (int q = 0; q < QN; ++q) {
-          const uint32_t m = 0u - ((SelWord(sw[q], r >> 5) >> (r & 31)) & 1u);
-          acc[q].x ^= v[u].x & m;
-          acc[q].y ^= v[u].y & m;
-          acc[q].z ^= v[u].z & m;
-          acc[q].w ^= v[u].w & m;
-        }
-      }
-    }
-  }
-  FoldPartials<QN>(a, acc, red, Cs, G, active, chunk_lo);
-}
-
-// Fast path for record widths of C = 64 / G chunks (G = 2..32 records per
-// wave-instruction) or C a multiple of 64 (G = 1, slices of 64 chunks).  The
-// records of one wave-instruction never straddle a 32-record selection word,
-// so each query's word is wave-uniform (SGPRs) and a lane's mask is one
-// signed bit-field extract; up to 16 queries per pass.
+// Masked XOR scan for any record width.  G records share a wave-instruction
+// (G a power of two): G = 1 for C > 32 chunks (64-chunk slices of a record
+// over gridDim.y, the last slice narrower), else the largest G with G * C <= 64
+// (whole records, Cs = C chunks each).  Lanes past G * Cs repeat a load of
+// their group and are dropped by FoldPartials.  For G <= 32 the records of one
+// wave-instruction never straddle a 32-record selection word, so each query's
+// word is wave-uniform (SGPRs) and a lane's mask is one signed bit-field
+// extract; G = 64 (16-byte records) picks the lane's word of a uniform pair.
+// The mask is applied with one v_bitop3 per dword; up to 16 queries per pass.
 template <int QN, int G>
 __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
-  constexpr int Cs = 64 / G;
-  constexpr int U = (G * 8 <= 32) ? 8 : 32 / G;  // loads in flight per lane
+  constexpr int U = (G >= 64) ? 2 : (G * 8 <= 32) ? 8 : 32 / G;  // loads in flight
   __shared__ uint4 red[kScanBlock];
   const int lane = threadIdx.x & 63;
   // wave-uniform by construction; readfirstlane lets the compiler see it, so
   // the selection words below are scalar loads into SGPRs
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int chunk_lo = blockIdx.y * 64;
-  const int my_chunk = chunk_lo + (lane % Cs);
-  const int my_rec = lane / Cs;
+  const int Cs = (G == 1) ? min(64, a.C - chunk_lo) : a.C;
+  const bool active = lane < G * Cs;
+  const int my_chunk = chunk_lo + lane % Cs;
+  const int my_rec = min(lane / Cs, G - 1);
   const uint32_t* sel = reinterpret_cast<const uint32_t*>(a.sel);
   uint4 acc[QN];
 #pragma unroll
@@ -245,39 +202,69 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
   for (int64_t tile = (int64_t)blockIdx.x * kScanWaves + wave; tile < tiles; tile += wstride) {
     const int64_t rec0 = tile << 7;
     const bool full = rec0 + 128 <= a.num_records;
-#pragma unroll 1
-    for (int d = 0; d < 4; ++d) {
-      // selection word d (records rec0 + 32d ..) of each query
-      uint32_t word[QN];
+    if constexpr (G == 64) {
+      // 128 records = 2 wave-instructions; lane l of half h is record
+      // rec0 + 64h + l, selection bit l & 31 of word 2h + (l >> 5).
+      uint4 v[U];
 #pragma unroll
-      for (int q = 0; q < QN; ++q)
-        word[q] = (q < a.nq) ? sel[((int64_t)(a.q0 + q) * a.sel_blocks + tile) * 4 + d] : 0u;
-#pragma unroll 1
-      for (int k0 = 0; k0 < 32; k0 += G * U) {
-        uint4 v[U];
+      for (int h = 0; h < U; ++h) {
+        const int64_t rec = rec0 + 64 * h + lane;
+        v[h] = (full || rec < a.num_records) ? LoadRecordWord(&a.db[rec])
+                                              : make_uint4(0, 0, 0, 0);
+      }
+      const bool upper = lane >= 32;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int64_t rec = rec0 + d * 32 + k0 + u * G + my_rec;
-          v[u] = (full || rec < a.num_records) ? LoadRecordWord(&a.db[rec * a.C + my_chunk])
-                                                : make_uint4(0, 0, 0, 0);
+      for (int q = 0; q < QN; ++q) {
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        if (q < a.nq) {
+#pragma unroll
+          for (int d = 0; d < 4; ++d) w[d] = sel[((int64_t)(a.q0 + q) * a.sel_blocks + tile) * 4 + d];
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int bit = k0 + u * G + my_rec;
+        for (int h = 0; h < U; ++h) {
+          const uint32_t word = upper ? w[2 * h + 1] : w[2 * h];
+          const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)word, lane & 31, 1);
+          acc[q].x = __builtin_amdgcn_bitop3_b32(acc[q].x, v[h].x, m, 0x78);
+          acc[q].y = __builtin_amdgcn_bitop3_b32(acc[q].y, v[h].y, m, 0x78);
+          acc[q].z = __builtin_amdgcn_bitop3_b32(acc[q].z, v[h].z, m, 0x78);
+          acc[q].w = __builtin_amdgcn_bitop3_b32(acc[q].w, v[h].w, m, 0x78);
+        }
+      }
+    } else {
+#pragma unroll 1
+      for (int d = 0; d < 4; ++d) {
+        // selection word d (records rec0 + 32d ..) of each query
+        uint32_t word[QN];
 #pragma unroll
-          for (int q = 0; q < QN; ++q) {
-            const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)word[q], bit, 1);
-            // acc ^= v & m as one v_bitop3 (truth table src0 ^ (src1 & src2))
-            acc[q].x = __builtin_amdgcn_bitop3_b32(acc[q].x, v[u].x, m, 0x78);
-            acc[q].y = __builtin_amdgcn_bitop3_b32(acc[q].y, v[u].y, m, 0x78);
-            acc[q].z = __builtin_amdgcn_bitop3_b32(acc[q].z, v[u].z, m, 0x78);
-            acc[q].w = __builtin_amdgcn_bitop3_b32(acc[q].w, v[u].w, m, 0x78);
+        for (int q = 0; q < QN; ++q)
+          word[q] = (q < a.nq) ? sel[((int64_t)(a.q0 + q) * a.sel_blocks + tile) * 4 + d] : 0u;
+#pragma unroll 1
+        for (int k0 = 0; k0 < 32; k0 += G * U) {
+          uint4 v[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int64_t rec = rec0 + d * 32 + k0 + u * G + my_rec;
+            v[u] = (full || rec < a.num_records) ? LoadRecordWord(&a.db[rec * a.C + my_chunk])
+                                                  : make_uint4(0, 0, 0, 0);
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int bit = k0 + u * G + my_rec;
+#pragma unroll
+            for (int q = 0; q < QN; ++q) {
+              const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)word[q], bit, 1);
+              // acc ^= v & m as one v_bitop3 (truth table src0 ^ (src1 & src2))
+              acc[q].x = __builtin_amdgcn_bitop3_b32(acc[q].x, v[u].x, m, 0x78);
+              acc[q].y = __builtin_amdgcn_bitop3_b32(acc[q].y, v[u].y, m, 0x78);
+              acc[q].z = __builtin_amdgcn_bitop3_b32(acc[q].z, v[u].z, m, 0x78);
+              acc[q].w = __builtin_amdgcn_bitop3_b32(acc[q].w, v[u].w, m, 0x78);
+            }
           }
         }
       }
     }
   }
-  FoldPartials<QN>(a, acc, red, Cs, G, true, chunk_lo);
+  FoldPartials<QN>(a, acc, red, Cs, G, active, chunk_lo);
 }
 
 int LaunchGatherRows(int grid, hipStream_t st, int64_t n, const int64_t* src_offset,
@@ -327,17 +314,10 @@ static void LaunchScanG(int nq, dim3 g, hipStream_t st, const ScanArgs& a) {
 }
 
 int PirScanGroup(int C) {
-  if (C % 64 == 0) return 1;
-  switch (C) {
-    case 2:
-    case 4:
-    case 8:
-    case 16:
-    case 32:
-      return 64 / C;
-    default:
-      return 0;
-  }
+  if (C > 32) return 1;
+  int g = 1;
+  while (g * 2 * C <= 64) g *= 2;
+  return g;
 }
 
 int LaunchPirScan(int nq, dim3 g, hipStream_t st, const ScanArgs& a) {
@@ -361,14 +341,7 @@ int LaunchPirScan(int nq, dim3 g, hipStream_t st, const ScanArgs& a) {
       LaunchScanG<32>(nq, g, st, a);
       break;
     default:
-      if (nq == 1)
-        hipLaunchKernelGGL((KPirScan<1>), g, dim3(kScanBlock), 0, st, a);
-      else if (nq <= 2)
-        hipLaunchKernelGGL((KPirScan<2>), g, dim3(kScanBlock), 0, st, a);
-      else if (nq <= 4)
-        hipLaunchKernelGGL((KPirScan<4>), g, dim3(kScanBlock), 0, st, a);
-      else
-        hipLaunchKernelGGL((KPirScan<8>), g, dim3(kScanBlock), 0, st, a);
+      LaunchScanG<64>(nq, g, st, a);
   }
   return LaunchCheck("pir scan kernel launch");
 }

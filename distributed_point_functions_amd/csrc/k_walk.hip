@@ -83,7 +83,12 @@ __device__ __forceinline__ void WalkPoints(const WalkArgs& w, Walk<NP>& s, const
     s.x[n][2] = v.z;
     s.x[n][3] = v.w;
     s.t[n] = w.cb_in[s.src[n]];
-    p[n] = w.paths[s.idx[n]];
+    if (w.paths) {
+      p[n] = w.paths[s.idx[n]];
+    } else {  // implicit paths: point j of each key is tree index j
+      const uint64_t j = (uint64_t)(ppk > 0 ? s.idx[n] - s.src[n] * ppk : s.idx[n]);
+      p[n] = make_uint4((uint32_t)j, (uint32_t)(j >> 32), 0u, 0u);
+    }
   }
   for (int level = 0; level < w.num_levels; ++level) {
     const int bi = w.num_levels - level - 1 + w.rightshift;

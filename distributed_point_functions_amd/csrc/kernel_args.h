@@ -103,7 +103,6 @@ constexpr int kPointsWaves = DPF_POINTS_WAVES;
 
 constexpr int kScanBlock = 256;
 constexpr int kScanWaves = kScanBlock / 64;
-constexpr int kScanUnroll = 8;
 constexpr int kFoldWords = 4;
 constexpr int kFoldSlices = 64;
 
@@ -155,9 +154,9 @@ int LaunchXorFold(unsigned blocks, hipStream_t st, const uint4* parts, int num_p
 int LaunchXorFoldBytes(int grid, hipStream_t st, const uint8_t* parts, int num_parts,
                        int64_t bytes, uint8_t* out);
 int LaunchPirScan(int nq, dim3 grid, hipStream_t st, const ScanArgs& a);
-// Records per wave-instruction of the fast scan for C chunks per record
-// (0 = generic scan); queries per scan pass = PirScanQueries(C).
+// Records per wave-instruction of KPirScanG for C chunks per record;
+// queries per scan pass = PirScanQueries(C).
 int PirScanGroup(int C);
-inline int PirScanQueries(int C) { return PirScanGroup(C) ? 16 : 8; }
+inline int PirScanQueries(int) { return 16; }
 
 }  // namespace dpf_amd

@@ -4,8 +4,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <cstdlib>
-#include <cstring>
 #include <cmath>
 
 #include "dpf_amd/dense_dpf_pir_server.h"
@@ -39,34 +37,6 @@ hipStream_t PirStream() {
 // AlignBytes (pir/dense_dpf_pir_database.cc:40-52).
 int64_t AlignBytes(int64_t n) { return (n + 15) & ~int64_t{15}; }
 
-static int64_t ScanFriendlyStride(int64_t stride) {
-  const int64_t c = stride / 16;
-  if (c >= 64) return ((c + 63) / 64) * 64 * 16;
-  int64_t p = 1;
-  while (p < c) p <<= 1;
-  return (p < 2 ? 2 : p) * 16;  // one 16-byte chunk per record has no G path
-}
-
-// Device row stride of a database of n records whose 16-byte-aligned size
-// is `aligned`: the scan-friendly width only when it costs at most 25 % more
-// bytes (240 -> 256 B yes; 16 -> 32 B or 1040 -> 2048 B no: the scan is
-// HBM-bound and would read the padding) and the padded table leaves a
-// reserve of free HBM for the per-request workspaces.  DPF_AMD_PIR_STRIDE=
-// aligned / padded forces either choice (tests, A/B measurements).
-static int64_t ChooseStride(int64_t aligned, int64_t n) {
-  const int64_t padded = ScanFriendlyStride(aligned);
-  if (padded == aligned) return aligned;
-  const char* force = std::getenv("DPF_AMD_PIR_STRIDE");
-  if (force && std::strcmp(force, "aligned") == 0) return aligned;
-  const bool forced_padded = force && std::strcmp(force, "padded") == 0;
-  if (!forced_padded && padded * 4 > aligned * 5) return aligned;
-  size_t free_bytes = 0, total_bytes = 0;
-  if (hipMemGetInfo(&free_bytes, &total_bytes) == hipSuccess) {
-    const int64_t reserve = std::max<int64_t>(int64_t{1} << 30, (int64_t)(total_bytes / 16));
-    if (n * padded + reserve > (int64_t)free_bytes) return aligned;
-  }
-  return padded;
-}
 
 }  // namespace
 
@@ -123,22 +93,11 @@ StatusOr<std::unique_ptr<DenseDpfPirDatabase::Interface>> DenseDpfPirDatabase::B
   for (const std::string& v : values_) max_size = std::max<int64_t>(max_size, v.size());
   db->num_records_ = n;
   db->max_value_size_ = max_size;
-  // Device row stride: the reference's 16-byte alignment, or a width the
-  // wave-uniform KPirScanG path handles (32, 64, 128, 256, 512 B or a
-  // multiple of 1 KiB; PirScanGroup) when ChooseStride allows it (e.g.
-  // 240-byte cuckoo values -> 256 B).  Responses are still max_value_size_
-  // bytes.  If the padded allocation fails anyway, the aligned stride is used.
-  const int64_t aligned = std::max<int64_t>(16, AlignBytes(max_size));
-  db->stride_ = ChooseStride(aligned, n);
-  int64_t bytes = std::max<int64_t>(16, n * db->stride_);
-  if (db->stride_ != aligned && hipMalloc(&db->records_, bytes) != hipSuccess) {
-    (void)hipGetLastError();  // clear the failed allocation's sticky error
-    db->records_ = nullptr;
-    db->stride_ = aligned;
-    bytes = std::max<int64_t>(16, n * db->stride_);
-  }
-  if (db->records_ == nullptr)
-    DPF_RETURN_IF_ERROR(HipStatus(hipMalloc(&db->records_, bytes), "hipMalloc(database)"));
+  // Device row stride: the reference's 16-byte alignment (KPirScanG maps any
+  // width onto the wave, so no padding is read or stored).
+  db->stride_ = std::max<int64_t>(16, AlignBytes(max_size));
+  const int64_t bytes = std::max<int64_t>(16, n * db->stride_);
+  DPF_RETURN_IF_ERROR(HipStatus(hipMalloc(&db->records_, bytes), "hipMalloc(database)"));
   DPF_RETURN_IF_ERROR(HipStatus(hipMemset(db->records_, 0, bytes), "hipMemset(database)"));
   // Upload in 64 MiB chunks of zero-padded fixed-stride rows.
   const int64_t rows_per_chunk = std::max<int64_t>(1, (64 << 20) / db->stride_);
@@ -423,10 +382,10 @@ StatusOr<PirResponse> DenseDpfPirServer::HandlePlainRequest(const PirRequest& re
     void* sel = nullptr;
     DPF_RETURN_IF_ERROR(HipStatus(hipMallocAsync(&sel, 16 * blocks * q, s), "alloc"));
     const dpf_amd_value_type layout = dpf_internal::HostLayoutOf<XorWrapper<uint128>>();
-    Status st;
-    for (int i = 0; i < q && st.ok(); ++i)
-      st = dpf_->ExpandLeavesOnDevice(plain.dpf_key(i), 0, blocks, layout,
-                                      static_cast<char*>(sel) + 16 * blocks * i, s);
+    std::vector<const DpfKey*> keys(q);
+    for (int i = 0; i < q; ++i) keys[i] = &plain.dpf_key(i);
+    Status st = dpf_->ExpandLeavesOnDeviceBatched(
+        Span<const DpfKey* const>(keys.data(), keys.size()), blocks, layout, sel, s);
     StatusOr<std::vector<std::string>> r =
         st.ok() ? gpu_db->InnerProductWithDevice(sel, blocks, q, s)
                 : StatusOr<std::vector<std::string>>(st);

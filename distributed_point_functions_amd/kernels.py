@@ -141,10 +141,10 @@ def evaluate_points_batched(num_keys: int, points_per_key: int, key_seeds, key_c
                             key_value_corrections=None, value_correction_all=(), out=None):
     """Batched EvaluateAt over num_keys keys (dpf_amd_evaluate_points_batched):
     point k * points_per_key + j belongs to key k; correction words are
-    [key][level] arrays."""
+    [key][level] arrays; paths None = point j of each key is tree index j."""
     n = num_keys * points_per_key
     if out is None:
-        out = torch.empty(n * desc.out_stride, dtype=torch.uint8, device=paths.device)
+        out = torch.empty(n * desc.out_stride, dtype=torch.uint8, device=key_seeds.device)
     corr = _corr_words(value_correction_all)
     check(_lib.lib().dpf_amd_evaluate_points_batched(
         num_keys, points_per_key, dptr(key_seeds), dptr(key_control_bits), dptr(paths),

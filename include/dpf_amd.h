@@ -117,6 +117,8 @@ int dpf_amd_evaluate_seeds(int64_t num_seeds, int num_levels,
  * are produced, element e (< corrected_elements_per_block) of leaf g being
  * written in host layout at
  *   out + ((g - leaf_begin) * cepb + e) * vt->out_stride.
+ * Only the scalars are written: padding bytes of a host layout with holes
+ * keep their previous contents (the Tier-2 API clears them first).
  * Correction words for the num_levels levels are device arrays; the value
  * correction (epb * num_scalars words of 128 bits, flattened per element)
  * and the party are host values (h:815-827, 856-858). */
@@ -161,8 +163,9 @@ int dpf_amd_evaluate_points(
  * key_seeds, key_control_bits, key_party (NULL = `party_all`),
  * key_value_corrections (epb * num_scalars words per key; NULL =
  * `value_correction_all`), and the correction words laid out [key][level]
- * (num_keys * num_levels each).  Per-point: paths, block_index (NULL = 0),
- * out (one host-layout T per point). */
+ * (num_keys * num_levels each).  Per-point: paths (NULL = point j of each
+ * key walks to tree index j: the first points_per_key leaves of every key),
+ * block_index (NULL = 0), out (one host-layout T per point). */
 int dpf_amd_evaluate_points_batched(
     int64_t num_keys, int64_t points_per_key, const void* key_seeds,
     const uint8_t* key_control_bits, const void* paths, int paths_rightshift,

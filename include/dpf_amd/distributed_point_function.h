@@ -235,6 +235,13 @@ class DistributedPointFunction {
   // writing host-layout values to device memory `out` (bench / sharding).
   Status ExpandLeavesOnDevice(const DpfKey& key, int64_t leaf_begin, int64_t leaf_end,
                               const dpf_amd_value_type& vt, void* out, void* stream) const;
+  // Leaves [0, num_leaves) of every key, key i's at out + i * num_leaves *
+  // cepb * out_stride (the selection vectors of a batched PIR request).  Small
+  // batches take one upload and one launch (per-leaf walks); large ones one
+  // tree expansion per key.
+  Status ExpandLeavesOnDeviceBatched(Span<const DpfKey* const> keys, int64_t num_leaves,
+                                     const dpf_amd_value_type& vt, void* out,
+                                     void* stream) const;
 
  private:
   explicit DistributedPointFunction(std::unique_ptr<dpf_internal::DpfState> state);

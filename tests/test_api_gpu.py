@@ -197,12 +197,13 @@ def test_pir_database_inner_product_vs_oracle(api, n, size):
     assert db.inner_product_with(sels) == po.inner_product(records, sels)
 
 
-@pytest.mark.parametrize("size,default,padded", [(16, 16, 32), (64, 64, 64), (240, 256, 256),
-                                                 (1040, 1040, 2048), (100, 128, 128), (200, 208, 256)])
-def test_pir_database_stride_choice_and_forced_strides(api, monkeypatch, size, default, padded):
-    """Builder's device stride (pir.cc ChooseStride): padded to a KPirScanG
-    width only within 25 % and an HBM budget; DPF_AMD_PIR_STRIDE forces either
-    layout, and every layout answers as the oracle."""
+@pytest.mark.parametrize("size", [1, 16, 17, 32, 40, 80, 200, 240, 272, 500, 528, 1008, 1040,
+                                  2064])
+def test_pir_database_every_record_width(api, size):
+    """KPirScanG maps every 16-byte-aligned width onto the wave (G = 64 ..
+    1 records per wave-instruction, idle lanes, 64-chunk slices with a narrow
+    tail): rows are stored at the reference's alignment, no padding, and 1,
+    16 and 20 queries (two passes) answer as the oracle on a ragged last tile."""
     _, _, P = api
     n = 3001
     records = _records(n, size, size)
@@ -210,19 +211,14 @@ def test_pir_database_stride_choice_and_forced_strides(api, monkeypatch, size, d
     rng = random.Random(size)
     sels = [[rng.getrandbits(128) for _ in range((n + 127) // 128)] for _ in range(20)]
     want = po.inner_product(records, sels)
-    aligned = (size + 15) // 16 * 16
-    for force, stride in ((None, default), ("aligned", aligned), ("padded", padded)):
-        if force:
-            monkeypatch.setenv("DPF_AMD_PIR_STRIDE", force)
-        else:
-            monkeypatch.delenv("DPF_AMD_PIR_STRIDE", raising=False)
-        db = P.DenseDpfPirDatabase()
-        db.insert_fixed(arr)
-        db.build()
-        assert db.record_stride == stride, force
-        assert db.max_value_size == size
-        assert db.inner_product_with(sels) == want, force
-        assert db.inner_product_with(sels[:1]) == want[:1], force
+    db = P.DenseDpfPirDatabase()
+    db.insert_fixed(arr)
+    db.build()
+    assert db.record_stride == (size + 15) // 16 * 16
+    assert db.max_value_size == size
+    assert db.inner_product_with(sels) == want
+    assert db.inner_product_with(sels[:16]) == want[:16]
+    assert db.inner_product_with(sels[:1]) == want[:1]
 
 
 def _pir_setup(api, n, size, seed=0):

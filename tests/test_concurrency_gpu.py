@@ -54,6 +54,30 @@ def test_dpf_evaluate_concurrently_from_1024_threads(cuda):
     assert all(_run_threads(call))
 
 
+def test_host_layout_padding_bytes_are_zero(cuda):
+    """Rows of a host layout with holes ({u32, u64}: 4 unused bytes) carry
+    zeros there, never stale device memory (host_device.h ClearPadding)."""
+    import torch
+    from distributed_point_functions_amd import value_types as V
+    from distributed_point_functions_amd.dpf import DistributedPointFunction, DpfParameters
+    # leave non-zero garbage in the stream-ordered pools first
+    junk = torch.full((1 << 24,), 0xAB, dtype=torch.uint8, device=cuda)
+    del junk
+    vt = V.Tuple(V.Integer(32), V.IntModN(64, 2 ** 64 - 59))
+    dpf = DistributedPointFunction.create(DpfParameters(12, vt, 48))
+    k0, _ = dpf.generate_keys(77, (5, 6), seeds=(1, 2))
+    outs = [dpf.evaluate_next([], dpf.create_evaluation_context(k0), raw=True),
+            dpf.evaluate_at(k0, 0, list(range(0, 4096, 7)), raw=True)]
+    for raw in outs:
+        covered = np.zeros(raw.dtype.itemsize, bool)
+        for name in raw.dtype.names:
+            dt, off = raw.dtype.fields[name][:2]
+            covered[off:off + dt.itemsize] = True
+        assert not covered.all()
+        rows = raw.view(np.uint8).reshape(len(raw), raw.dtype.itemsize)
+        assert not rows[:, ~covered].any()
+
+
 def test_pir_server_handle_request_from_1024_threads(cuda):
     from distributed_point_functions_amd import pir as P
     from distributed_point_functions_amd import value_types as V

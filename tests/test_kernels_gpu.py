@@ -284,6 +284,41 @@ def test_evaluate_points_batched_matches_oracle(K, cuda, spec, ld, nkeys, ppk):
         assert [got[k * ppk + j] for j in sample] == want, k
 
 
+@pytest.mark.parametrize("ld,nkeys,ppk", [(7, 3, 128), (21, 15, 12288), (12, 2, 1000)])
+def test_evaluate_points_batched_implicit_paths(K, cuda, ld, nkeys, ppk):
+    """paths = NULL walks point j of every key to tree index j (the batched
+    PIR selection expansion): equal to explicit paths, and to the oracle's
+    full-domain expansion of each key's first ppk leaves."""
+    import torch
+    spec = ("xor", 128)
+    from distributed_point_functions_amd import value_types as vtm
+    vt = vtm.from_spec(spec)
+    keys = []
+    for k in range(nkeys):
+        d, k0, k1, _, _ = _keys(spec, ld, seed=k + 40)
+        keys.append((d, (k0, k1)[k % 2]))
+    d = keys[0][0]
+    L = d.hierarchy_to_tree(0)
+    ks = [k for _, k in keys]
+    args = (K.u128_tensor([k.seed for k in ks], cuda), u8([k.party for k in ks], cuda))
+    rest = dict(key_party=torch.tensor([k.party for k in ks], dtype=torch.int8, device=cuda),
+                key_value_corrections=K.u128_tensor(
+                    [c for k in ks for c in k.value_corrections()[0]], cuda))
+    cw = (K.u128_tensor([c for k in ks for c in (k.cw_seeds()[:L] or [0])], cuda),
+          u8([c for k in ks for c in (k.ccl()[:L] or [0])], cuda),
+          u8([c for k in ks for c in (k.ccr()[:L] or [0])], cuda))
+    desc = vt.descriptor(d.blocks_needed(0))
+    implicit = K.evaluate_points_batched(nkeys, ppk, *args, None, 0, L, *cw, desc, **rest)
+    explicit = K.evaluate_points_batched(nkeys, ppk, *args,
+                                         K.u128_tensor(list(range(ppk)) * nkeys, cuda), 0, L,
+                                         *cw, desc, **rest)
+    assert torch.equal(implicit, explicit)
+    got = implicit.cpu().numpy().view(np.uint64).reshape(nkeys, ppk, 2)
+    for k in (0, nkeys - 1):
+        full = keys[k][0].expand_subtree_words(ks[k], 0, L)
+        assert np.array_equal(got[k], full.reshape(-1, 2)[:ppk]), k
+
+
 @pytest.mark.parametrize("stride,opp", [(1, 32), (2, 8), (4, 4), (8, 256), (8, 3), (16, 5),
                                         (24, 7), (32, 64), (12, 4)])
 def test_gather_rows(K, cuda, stride, opp):

@@ -27,20 +27,31 @@ def fx():
 
 
 def test_pir_server_answers_protobuf_request(cuda, fx):
+    """A PirRequest built and serialized by google.protobuf (PlainRequest with
+    both parties' keys for one index) answered by the native server; the
+    response is canonical protobuf and its two masked responses XOR to the
+    record."""
     from distributed_point_functions_amd import pir as P
-    p = fx["pir"]
-    case = next(c for c in fx["keys"] if c["name"] == "xor128")
-    ld, alpha = case["levels"][0][0], int(case["alpha"])
-    n = 1 << ld
+    from distributed_point_functions_amd import value_types as V
+    from distributed_point_functions_amd.dpf import DistributedPointFunction, DpfParameters
+    n, idx = 3000, 2077
     records = np.random.default_rng(11).integers(0, 256, (n, 40), dtype=np.uint8)
     db = P.DenseDpfPirDatabase()
     db.insert_fixed(records)
     server = P.DenseDpfPirServer.create_plain(n, db)
-    resp = server.handle_request(bytes.fromhex(p["plain_request"]))
+    dpf = DistributedPointFunction.create(DpfParameters((n - 1).bit_length(), V.XorWrapper(128)))
+    (k0, k1), = P.client_keys(dpf, n, [idx], seeds=[(5, 6)])
+    req = W.cls("PirRequest")()
+    for k in (k0, k1):
+        req.dpf_pir_request.plain_request.dpf_key.add().ParseFromString(bytes(k))
+    data = req.SerializeToString(deterministic=True)
+    assert data.hex() != fx["pir"]["plain_request"]
+    assert data == P.pir_request_plain([k0, k1])
+    resp = server.handle_request(data)
     assert W.canonical("PirResponse", resp) == resp
     m = W.cls("PirResponse").FromString(resp)
     r0, r1 = m.dpf_pir_response.masked_response
-    assert bytes(a ^ b for a, b in zip(r0, r1)) == records[alpha].tobytes()
+    assert bytes(a ^ b for a, b in zip(r0, r1)) == records[idx].tobytes()
 
 
 @pytest.mark.parametrize("name", ["incremental_u32", "incremental_mixed"])

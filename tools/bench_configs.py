@@ -281,6 +281,41 @@ def c4q(dev, reps):
     return res
 
 
+def stride(dev, reps):
+    """Dense scan at 2^26 rows with the reference's 16-byte-aligned row
+    stride vs the same rows padded to a power-of-two / 1 KiB-multiple width,
+    for 16 B and 1040 B records (why the builder stores rows
+    unpadded)."""
+    n = 1 << 26
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(9)
+    res = {"config": "stride", "workload": "XOR scan 2^26 rows, aligned vs padded stride"}
+    for rec, aligned, padded in ((16, 16, 32), (1040, 1040, 2048)):
+        db_a = torch.randint(0, 256, (n, aligned), dtype=torch.uint8, device=dev, generator=gen)
+        db_p = torch.zeros((n, padded), dtype=torch.uint8, device=dev)
+        db_p[:, :aligned] = db_a
+        for q in (1, 16):
+            sel = torch.randint(-2**63, 2**63 - 1, (q * (n // 128), 2), dtype=torch.int64,
+                                device=dev, generator=gen)
+            outs = []
+            for name, db, st in (("aligned", db_a, aligned), ("padded", db_p, padded)):
+                ws = torch.empty(max(16, _lib.lib().dpf_amd_inner_product_workspace_size(n, st, q)),
+                                 dtype=torch.uint8, device=dev)
+                out = torch.empty((q, st), dtype=torch.uint8, device=dev)
+                t = ev_time(lambda: kernels.inner_product(db.view(-1), n, st, sel, q, ws,
+                                                          out.view(-1)), reps)
+                outs.append(out[:, :rec].clone())
+                key = "r%d_%s_q%d" % (rec, name, q)
+                res[key + "_ms"] = t * 1e3
+                res[key + "_record_GBps"] = n * rec / t / 1e9
+                del ws
+            res["r%d_q%d_equal" % (rec, q)] = bool(torch.equal(outs[0], outs[1]))
+        res["r%d_table_GB" % rec] = {"aligned": n * aligned / 1e9, "padded": n * padded / 1e9}
+        del db_a, db_p
+        torch.cuda.empty_cache()
+    return res
+
+
 def dcf(dev, reps):
     from distributed_point_functions_amd.dcf import DcfParameters, DistributedComparisonFunction
     rng = random.Random(5)

@@ -1,0 +1,199 @@
+// cpp_api_bench.cc — wall-clock cost of the reference's C++ API on the
+// BASELINE configs c1-c3, called exactly as a C++ caller of
+// dpf/distributed_point_function.h would (host std::vector results), linked
+// against libdpf_amd.so.  One JSON line per config on stdout.
+//
+//   c1  EvaluateNext<uint64_t> full domain, log_domain_size 20
+//   c2  EvaluateAt<uint128> of 16384 random points for each of 64 keys,
+//       log_domain_size 128 (2^20 points)
+//   c3  16 hierarchy levels of 8 bits, uint64, EvaluateNext on 2^16 distinct
+//       surviving prefixes per level (distributed_point_function_benchmark.cc:
+//       154-191 shape)
+//
+// Built by distributed_point_functions_amd/build_native.py next to the
+// library; run on the GPU box: _native/cpp_api_bench [reps].
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <set>
+#include <vector>
+
+#include "dpf_amd/distributed_point_function.h"
+
+using namespace distributed_point_functions;
+
+namespace {
+
+double Now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+#define OK_OR_DIE(expr)                                                            \
+  do {                                                                             \
+    if (!(expr).ok()) {                                                            \
+      std::fprintf(stderr, "%s:%d: %s\n", __FILE__, __LINE__,                      \
+                   (expr).status().ToString().c_str());                            \
+      std::exit(1);                                                                \
+    }                                                                              \
+  } while (0)
+
+void C1(int reps) {
+  DpfParameters p;
+  p.set_log_domain_size(20);
+  p.mutable_value_type()->mutable_integer()->set_bitsize(64);
+  auto dpf = DistributedPointFunction::Create(p);
+  OK_OR_DIE(dpf);
+  auto keys = (*dpf)->GenerateKeys(uint128{777777}, uint128{123456789123ull});
+  OK_OR_DIE(keys);
+  double best = 1e30, total = 0;
+  bool ok = true;
+  for (int r = 0; r <= reps; ++r) {
+    auto ctx = (*dpf)->CreateEvaluationContext(keys->first);
+    OK_OR_DIE(ctx);
+    const double t0 = Now();
+    auto out = (*dpf)->EvaluateNext<uint64_t>(Span<const uint128>(), *ctx);
+    const double t = Now() - t0;
+    OK_OR_DIE(out);
+    ok &= out->size() == (size_t{1} << 20);
+    if (r > 0) {  // the first call warms up
+      best = std::min(best, t);
+      total += t;
+    }
+  }
+  std::printf("{\"config\": \"c1\", \"api\": \"C++ EvaluateNext<uint64_t> -> std::vector\", "
+              "\"leaves\": %d, \"best_ms\": %.4f, \"mean_ms\": %.4f, "
+              "\"leaves_per_s\": %.4g, \"correct\": %s}\n",
+              1 << 20, 1e3 * best, 1e3 * total / reps, (1 << 20) / best, ok ? "true" : "false");
+}
+
+void C2(int reps) {
+  DpfParameters p;
+  p.set_log_domain_size(128);
+  p.mutable_value_type()->mutable_integer()->set_bitsize(128);
+  auto dpf = DistributedPointFunction::Create(p);
+  OK_OR_DIE(dpf);
+  std::mt19937_64 rng(2);
+  const int nkeys = 64, per = 1 << 14;
+  std::vector<DpfKey> k0s, k1s;
+  std::vector<std::vector<uint128>> pts(nkeys);
+  std::vector<uint128> betas;
+  for (int k = 0; k < nkeys; ++k) {
+    const uint128 alpha = MakeUint128(rng(), rng()), beta = MakeUint128(rng(), rng());
+    auto keys = (*dpf)->GenerateKeys(alpha, beta);
+    OK_OR_DIE(keys);
+    k0s.push_back(keys->first);
+    k1s.push_back(keys->second);
+    betas.push_back(beta);
+    pts[k].resize(per);
+    for (auto& x : pts[k]) x = MakeUint128(rng(), rng());
+    pts[k][0] = alpha;
+  }
+  double best = 1e30;
+  for (int r = 0; r <= reps; ++r) {
+    const double t0 = Now();
+    for (int k = 0; k < nkeys; ++k) {
+      auto out = (*dpf)->EvaluateAt<uint128>(k0s[k], 0, pts[k]);
+      OK_OR_DIE(out);
+    }
+    const double t = Now() - t0;
+    if (r > 0) best = std::min(best, t);
+  }
+  bool ok = true;
+  for (int k = 0; k < nkeys; k += 9) {
+    auto a = (*dpf)->EvaluateAt<uint128>(k0s[k], 0, pts[k]);
+    auto b = (*dpf)->EvaluateAt<uint128>(k1s[k], 0, pts[k]);
+    OK_OR_DIE(a);
+    OK_OR_DIE(b);
+    ok &= uint128((*a)[0] + (*b)[0]) == betas[k] && uint128((*a)[1] + (*b)[1]) == 0;
+  }
+  std::printf("{\"config\": \"c2\", \"api\": \"C++ EvaluateAt<uint128>, 64 keys x 16384 points\", "
+              "\"points\": %d, \"best_ms\": %.3f, \"points_per_s\": %.4g, \"correct\": %s}\n",
+              nkeys * per, 1e3 * best, nkeys * per / best, ok ? "true" : "false");
+}
+
+void C3(int reps) {
+  const int H = 16;
+  std::vector<DpfParameters> ps(H);
+  for (int i = 0; i < H; ++i) {
+    ps[i].set_log_domain_size(8 * (i + 1));
+    ps[i].mutable_value_type()->mutable_integer()->set_bitsize(64);
+  }
+  auto dpf = DistributedPointFunction::CreateIncremental(ps);
+  OK_OR_DIE(dpf);
+  std::mt19937_64 rng(3);
+  const uint128 alpha = MakeUint128(rng(), rng());
+  std::vector<uint128> betas(H);
+  for (auto& b : betas) b = rng();
+  auto keys = (*dpf)->GenerateKeysIncremental(alpha, betas);
+  OK_OR_DIE(keys);
+  // prefixes[i]: 2^16 distinct children of level i-1's prefixes, sorted,
+  // alpha's prefix included
+  std::vector<std::vector<uint128>> prefixes(H);
+  for (int i = 1; i < H; ++i) {
+    std::set<uint128> cur;
+    const uint128 ap = alpha >> (128 - 8 * i);
+    cur.insert(ap);
+    if (i == 1) {
+      for (int j = 0; j < 256; ++j) cur.insert(j);
+    } else {
+      const auto& prev = prefixes[i - 1];
+      while (cur.size() < (size_t{1} << 16))
+        cur.insert((prev[rng() % prev.size()] << 8) | (rng() & 255));
+    }
+    prefixes[i].assign(cur.begin(), cur.end());
+  }
+  std::vector<double> best(H, 1e30);
+  double best_total = 1e30;
+  size_t leaves = 0;
+  bool ok = true;
+  for (int r = 0; r <= reps; ++r) {
+    auto c0 = (*dpf)->CreateEvaluationContext(keys->first);
+    auto c1 = (*dpf)->CreateEvaluationContext(keys->second);
+    OK_OR_DIE(c0);
+    OK_OR_DIE(c1);
+    double total = 0;
+    leaves = 0;
+    for (int i = 0; i < H; ++i) {
+      const double t0 = Now();
+      auto a = (*dpf)->EvaluateNext<uint64_t>(prefixes[i], *c0);
+      const double t = Now() - t0;
+      OK_OR_DIE(a);
+      total += t;
+      leaves += a->size();
+      if (r > 0) best[i] = std::min(best[i], t);
+      if (r == 0) {  // check the share sum once
+        auto b = (*dpf)->EvaluateNext<uint64_t>(prefixes[i], *c1);
+        OK_OR_DIE(b);
+        size_t nonzero = 0;
+        for (size_t x = 0; x < a->size(); ++x) {
+          const uint64_t s = (*a)[x] + (*b)[x];
+          if (s != 0) {
+            ++nonzero;
+            ok &= s == static_cast<uint64_t>(betas[i]);
+          }
+        }
+        ok &= nonzero == 1;
+      }
+    }
+    if (r > 0) best_total = std::min(best_total, total);
+  }
+  std::printf("{\"config\": \"c3\", \"api\": \"C++ EvaluateNext<uint64_t> per level -> "
+              "std::vector\", \"levels\": %d, \"returned_leaves\": %zu, \"best_total_ms\": %.3f, "
+              "\"leaves_per_s\": %.4g, \"best_ms_per_level\": [",
+              H, leaves, 1e3 * best_total, leaves / best_total);
+  for (int i = 0; i < H; ++i) std::printf("%s%.3f", i ? ", " : "", 1e3 * best[i]);
+  std::printf("], \"correct\": %s}\n", ok ? "true" : "false");
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const int reps = argc > 1 ? std::atoi(argv[1]) : 5;
+  C1(reps);
+  C2(std::max(1, reps / 2));
+  C3(std::max(1, reps / 2));
+  return 0;
+}

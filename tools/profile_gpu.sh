@@ -8,6 +8,8 @@ ARGS=${@:-"--steps 3 --warmup 1 --skip-cpu-baseline"}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
+# the profiled library: bench.py trusts PMC traffic only for this exact build
+sha256sum ${DPF_AMD_LIB:-distributed_point_functions_amd/_native/libdpf_amd.so} | cut -d" " -f1 > $OUT/library.sha256
 run() {  # name, timeout, rocprof args...
   local name=$1 to=$2; shift 2
   timeout -k 10 $to rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 bench.py $ARGS > $OUT/$name.log 2>&1

@@ -48,6 +48,10 @@ def main(tag):
                 continue
             pmc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     out = {}
+    sha = os.path.join(src, "library.sha256")
+    if os.path.exists(sha):
+        # bench.py reports roofline.traffic only while this build is the one loaded
+        out["_meta"] = {"library_sha256": open(sha).read().strip()}
     for k, d in pmc.items():
         avg = {c: sum(v) / len(v) for c, v in d.items()}
         e = {"counters_per_launch": avg, "launches": max(len(v) for v in d.values())}
@@ -70,7 +74,8 @@ def main(tag):
              "`rocprofv3 --kernel-trace --stats`, then separate `--pmc` passes)." % tag, "",
              "| kernel | calls | avg ms | HBM read GB | HBM write GB | VALU wave-instr | LDS wave-instr | LDS bank conflicts |",
              "|---|---|---|---|---|---|---|---|"]
-    for k, e in sorted(out.items(), key=lambda kv: -kv[1].get("avg_duration_ns", 0)):
+    kernels = {k: e for k, e in out.items() if k != "_meta"}
+    for k, e in sorted(kernels.items(), key=lambda kv: -kv[1].get("avg_duration_ns", 0)):
         c = e["counters_per_launch"]
         lines.append("| `%s` | %s | %.3f | %.3f | %.3f | %.4g | %.4g | %.4g |" % (
             k[:90], e.get("calls_in_trace", "?"), e.get("avg_duration_ns", 0) / 1e6,
