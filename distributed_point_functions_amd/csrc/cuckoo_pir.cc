@@ -11,6 +11,7 @@
 #include <fstream>
 
 #include "dpf_amd/cuckoo_hashing_sparse_dpf_pir_server.h"
+#include "host_device.h"
 #include "internal.h"
 
 namespace distributed_point_functions {
@@ -485,7 +486,7 @@ StatusOr<PirResponse> CuckooHashingSparseDpfPirServer::HandlePlainRequest(
     const int64_t blocks = std::max<int64_t>(1, (buckets + 127) / 128);
     hipStream_t s = CuckooStream();
     void* sel = nullptr;
-    DPF_RETURN_IF_ERROR(HipStatus(hipMallocAsync(&sel, 16 * blocks * q, s), "alloc"));
+    DPF_RETURN_IF_ERROR(dpf_internal_host::DevicePool::Get().Alloc(16 * blocks * q, s, &sel));
     const dpf_amd_value_type layout = dpf_internal::HostLayoutOf<XorWrapper<uint128>>();
     std::vector<const DpfKey*> keys(q);
     for (int i = 0; i < q; ++i) keys[i] = &plain.dpf_key(i);
@@ -494,7 +495,7 @@ StatusOr<PirResponse> CuckooHashingSparseDpfPirServer::HandlePlainRequest(
     StatusOr<std::vector<Database::RecordType>> r =
         st.ok() ? gpu_db->InnerProductWithDevice(sel, blocks, q, s)
                 : StatusOr<std::vector<Database::RecordType>>(st);
-    (void)hipFreeAsync(sel, s);
+    dpf_internal_host::DevicePool::Get().Free(sel, s);
     (void)hipStreamSynchronize(s);
     if (!r.ok()) return r.status();
     inner_products = std::move(*r);

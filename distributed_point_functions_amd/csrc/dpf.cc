@@ -717,6 +717,7 @@ bool DistributedPointFunction::IsValueTypeRegistered(const ValueType& value_type
 // ---------------------------------------------------------------------------
 using dpf_internal_host::AbiStatus;
 using dpf_internal_host::ClearPadding;
+using dpf_internal_host::CopyToHost;
 using dpf_internal_host::DeviceBuffer;
 using dpf_internal_host::HipStatus;
 using dpf_internal_host::HostTrace;
@@ -1148,10 +1149,8 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
   trace.Mark("upload+walk_launch");
   ctx.clear_partial_evaluations();
   if (update_ctx && n > 0) {
-    DPF_RETURN_IF_ERROR(HipStatus(
-        hipMemcpyAsync(seeds.data(), seeds_dev->get(), 16 * n, hipMemcpyDeviceToHost, s), "d2h"));
-    DPF_RETURN_IF_ERROR(HipStatus(
-        hipMemcpyAsync(cbs.data(), cb_dev->get(), n, hipMemcpyDeviceToHost, s), "d2h"));
+    DPF_RETURN_IF_ERROR(CopyToHost(seeds.data(), seeds_dev->get(), 16 * n, s));
+    DPF_RETURN_IF_ERROR(CopyToHost(cbs.data(), cb_dev->get(), n, s));
     DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
     std::vector<PartialEvaluation>* pe = ctx.mutable_partial_evaluations();
     pe->resize(n);
@@ -1279,7 +1278,10 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   const int64_t expanded = (num_roots << levels) * cepb;
   const size_t stride = static_cast<size_t>(vt.out_stride);
 
-  DeviceBuffer staging, result;
+  DeviceBuffer staging, result, gather_err, src_dev;
+  int gather_flag = 0;
+  void* gather_src_dev = nullptr;
+  std::vector<int64_t> gather_src_host;
   void* expand_out = nullptr;
   if (prefixes.empty() && out_on_device) {
     expand_out = out;
@@ -1302,22 +1304,49 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
     for (int64_t i = 0; i < num_prefixes; ++i)
       src[i] = prefix_map[i].first * blocks_per_tree_prefix * cepb +
                prefix_map[i].second * outputs_per_prefix;
-    DeviceBuffer src_dev;
+    for (int64_t i = 0; i < num_prefixes; ++i)
+      if (src[i] < 0 || src[i] > expanded - outputs_per_prefix)
+        return InternalError("gather offset " + std::to_string(src[i]) + " of prefix " +
+                             std::to_string(i) + " outside the " + std::to_string(expanded) +
+                             " expanded outputs");
     DPF_RETURN_IF_ERROR(src_dev.Upload(src.data(), 8 * num_prefixes, s));
+    gather_src_dev = src_dev.get();
+    gather_src_host = src;
     if (out_on_device) {
       final_dev = out;
     } else {
       DPF_RETURN_IF_ERROR(result.Alloc(total * stride, s));
       final_dev = result.get();
     }
-    DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_gather_rows(num_prefixes, src_dev.as<int64_t>(),
-                                                      outputs_per_prefix, stride, expand_out,
-                                                      final_dev, s)));
+    DPF_RETURN_IF_ERROR(gather_err.Alloc(sizeof(int), s));
+    DPF_RETURN_IF_ERROR(HipStatus(hipMemsetAsync(gather_err.get(), 0, sizeof(int), s), "memset"));
+    DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_gather_rows_checked(
+        num_prefixes, src_dev.as<int64_t>(), outputs_per_prefix, stride, expand_out, expanded,
+        final_dev, gather_err.as<int>(), s)));
+    DPF_RETURN_IF_ERROR(CopyToHost(&gather_flag, gather_err.get(), sizeof(int), s));
   }
   if (!out_on_device)
-    DPF_RETURN_IF_ERROR(HipStatus(
-        hipMemcpyAsync(out, final_dev, total * stride, hipMemcpyDeviceToHost, s), "d2h"));
+    DPF_RETURN_IF_ERROR(CopyToHost(out, final_dev, total * stride, s));
   DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+  if (gather_flag) {  // the offsets were checked on the host: the device copy differs
+    std::string detail;
+    if (!prefixes.empty()) {
+      std::vector<int64_t> back(num_prefixes);
+      if (hipMemcpy(back.data(), gather_src_dev, 8 * num_prefixes, hipMemcpyDeviceToHost) ==
+          hipSuccess) {
+        int64_t bad = 0;
+        for (int64_t i = 0; i < num_prefixes; ++i) {
+          if (back[i] == gather_src_host[i]) continue;
+          if (bad++ < 6)
+            detail += " [" + std::to_string(i) + "] " + std::to_string(gather_src_host[i]) +
+                      "->" + std::to_string(back[i]);
+        }
+        detail = " (" + std::to_string(bad) + " of " + std::to_string(num_prefixes) +
+                 " differ:" + detail + ")";
+      }
+    }
+    return InternalError("gather offsets corrupted between host and device" + detail);
+  }
   trace.Mark("gather+copy+sync");
   ctx.set_previous_hierarchy_level(hierarchy_level);
   return OkStatus();
@@ -1385,8 +1414,7 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
       n, seeds.get(), cbs.as<uint8_t>(), paths.get(), 0, levels, levels, cws.get(),
       ccl.as<uint8_t>(), ccr.as<uint8_t>(), &vt, bi.as<uint8_t>(), nullptr, key.party(), nullptr,
       reinterpret_cast<const uint64_t*>(corr.data()), dout.get(), nullptr, nullptr, s)));
-  DPF_RETURN_IF_ERROR(HipStatus(
-      hipMemcpyAsync(out, dout.get(), n * vt.out_stride, hipMemcpyDeviceToHost, s), "d2h"));
+  DPF_RETURN_IF_ERROR(CopyToHost(out, dout.get(), n * vt.out_stride, s));
   DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
   if (ctx) ctx->set_previous_hierarchy_level(hierarchy_level);
   return OkStatus();
@@ -1468,9 +1496,8 @@ Status DistributedPointFunction::EvaluateAndApplyRaw(Span<const DpfKey* const> k
         static_cast<int64_t>(levels) * n, dcws.get(), dccl.as<uint8_t>(), dccr.as<uint8_t>(),
         &vt, dbi.as<uint8_t>(), pty.as<int8_t>(), 0, dcorr.get(), nullptr, dout.get(),
         seeds.get(), cbs.as<uint8_t>(), s)));
-    DPF_RETURN_IF_ERROR(HipStatus(hipMemcpyAsync(host_out + h * n * vt.out_stride, dout.get(),
-                                                 n * vt.out_stride, hipMemcpyDeviceToHost, s),
-                                  "d2h"));
+    DPF_RETURN_IF_ERROR(CopyToHost(host_out + h * n * vt.out_stride, dout.get(),
+                                                 n * vt.out_stride, s));
     DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
     *levels_done = h + 1;
     // h:1190-1196: stop as soon as `op` returns false (the remaining levels

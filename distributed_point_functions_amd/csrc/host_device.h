@@ -6,8 +6,14 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <map>
+#include <mutex>
+#include <unordered_map>
+#include <utility>
+#include <vector>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 
 #include "dpf_amd.h"
@@ -68,6 +74,14 @@ class HostTrace {
   std::chrono::steady_clock::time_point t_;
 };
 
+// Device-to-host copy on `s`.  DPF_AMD_SYNC_D2H=1 drains the stream before
+// the copy is issued (diagnostics of kernel -> copy ordering).
+inline Status CopyToHost(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  static const bool drain = std::getenv("DPF_AMD_SYNC_D2H") != nullptr;
+  if (drain) DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+  return HipStatus(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s), "d2h");
+}
+
 // Host layouts with holes (e.g. {uint32_t, uint64_t}: 16 bytes, 4 unused):
 // the kernels write only the scalars, so a buffer whose rows reach the caller
 // is cleared first and stale device memory never shows up in the padding.
@@ -82,6 +96,234 @@ inline Status ClearPadding(const dpf_amd_value_type& vt, void* p, size_t bytes, 
   return HipStatus(hipMemsetAsync(p, 0, bytes, s), "hipMemsetAsync");
 }
 
+// Pinned staging for host-to-device uploads: the Tier-2 paths upload locals
+// that go out of scope before the stream drains, so every upload is first
+// copied into a pinned slot (then a true async DMA); a slot is reused only
+// after the event recorded behind its copy.
+class UploadRing {
+ public:
+  UploadRing() = default;
+  UploadRing(const UploadRing&) = delete;
+  UploadRing& operator=(const UploadRing&) = delete;
+  ~UploadRing() {
+    for (Slot& sl : slots_) {
+      if (sl.done) {
+        (void)hipEventSynchronize(sl.done);
+        (void)hipEventDestroy(sl.done);
+      }
+      if (sl.host) (void)hipHostFree(sl.host);
+    }
+  }
+  Status Copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return OkStatus();
+    Slot& sl = slots_[next_];
+    next_ = (next_ + 1) % kSlots;
+    if (sl.done == nullptr)
+      DPF_RETURN_IF_ERROR(HipStatus(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming),
+                                    "hipEventCreate"));
+    else
+      DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(sl.done), "upload slot"));
+    if (sl.cap < bytes) {
+      if (sl.host) (void)hipHostFree(sl.host);
+      sl.host = nullptr;
+      sl.cap = 0;
+      size_t cap = 4096;
+      while (cap < bytes) cap <<= 1;
+      const unsigned flags = Mode() == kKernelCoherent
+                                 ? (hipHostMallocMapped | hipHostMallocCoherent)
+                                 : hipHostMallocMapped;
+      DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc(&sl.host, cap, flags), "hipHostMalloc"));
+      DPF_RETURN_IF_ERROR(
+          HipStatus(hipHostGetDevicePointer(&sl.dev, sl.host, 0), "hipHostGetDevicePointer"));
+      sl.cap = cap;
+    }
+    std::memcpy(sl.host, src, bytes);
+    if (Mode() == kSdma || Mode() == kSdmaSync) {
+      DPF_RETURN_IF_ERROR(
+          HipStatus(hipMemcpyAsync(dst, sl.host, bytes, hipMemcpyHostToDevice, s), "upload"));
+      if (Mode() == kSdmaSync) DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+    } else {
+      DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd::CopyFromMappedHost(dst, sl.dev, bytes, s)));
+    }
+    return HipStatus(hipEventRecord(sl.done, s), "hipEventRecord");
+  }
+
+ private:
+  // DPF_AMD_UPLOAD = sdma (default: hipMemcpyAsync from the pinned slot) |
+  // sdma_sync | kernel | kernel_coherent (a copy kernel reading the mapped
+  // slot) — diagnostics of the H2D path.
+  enum UploadMode { kKernel, kKernelCoherent, kSdma, kSdmaSync };
+  static UploadMode Mode() {
+    static const UploadMode m = [] {
+      const char* e = std::getenv("DPF_AMD_UPLOAD");
+      if (!e) return kSdma;
+      if (!std::strcmp(e, "kernel")) return kKernel;
+      if (!std::strcmp(e, "kernel_coherent")) return kKernelCoherent;
+      if (!std::strcmp(e, "sdma_sync")) return kSdmaSync;
+      return kSdma;
+    }();
+    return m;
+  }
+  static constexpr int kSlots = 16;
+  struct Slot {
+    void* host = nullptr;
+    void* dev = nullptr;  // device address of `host`
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+  };
+  Slot slots_[kSlots];
+  int next_ = 0;
+};
+
+inline UploadRing& ThreadUploadRing() {
+  thread_local UploadRing ring;
+  return ring;
+}
+
+// Caching device allocator with stream-ordered reuse, on top of hipMalloc.
+// The library does not use hipMallocAsync: with ROCm 7.2's runtime its pool
+// handed EvaluateUntil memory that kernels saw with wrong contents (c3 at
+// 2^16 prefixes: gather offsets out of range, or a wrong share at alpha at
+// hierarchy level 5 — also with kernels and copies serialized), while the
+// same binary on ROCm 7.0's runtime and on plain hipMalloc was bit-exact.
+// A freed block keeps an event recorded on the freeing stream; it is handed
+// out again at once on that stream (stream order covers the reuse) and on
+// any other stream once the event has completed.  Blocks stay cached (sizes
+// rounded to powers of two up to 1 MiB, 2 MiB multiples above) until an
+// allocation fails, which releases the idle ones and retries.
+class DevicePool {
+ public:
+  static DevicePool& Get() {
+    static DevicePool* pool = new DevicePool();  // never destroyed: no HIP calls at exit
+    return *pool;
+  }
+
+  Status Alloc(size_t bytes, hipStream_t s, void** out) {
+    const size_t size = Bucket(bytes);
+    int dev = 0;
+    DPF_RETURN_IF_ERROR(HipStatus(hipGetDevice(&dev), "hipGetDevice"));
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      auto range = free_.equal_range(std::make_pair(dev, size));
+      for (auto it = range.first; it != range.second; ++it) {
+        Block& b = it->second;
+        if (b.stream != s && hipEventQuery(b.ready) != hipSuccess) continue;
+        *out = b.p;
+        events_.push_back(b.ready);
+        live_[b.p] = std::make_pair(size, dev);
+        cached_ -= size;
+        free_.erase(it);
+        return OkStatus();
+      }
+    }
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, size);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      Release();
+      e = hipMalloc(&p, size);
+    }
+    DPF_RETURN_IF_ERROR(HipStatus(e, "hipMalloc"));
+    std::lock_guard<std::mutex> l(mu_);
+    live_[p] = std::make_pair(size, dev);
+    *out = p;
+    return OkStatus();
+  }
+
+  void Free(void* p, hipStream_t s) {
+    if (p == nullptr) return;
+    std::lock_guard<std::mutex> l(mu_);
+    auto it = live_.find(p);
+    if (it == live_.end()) return;
+    Block b{p, it->second.first, s, nullptr};
+    const int dev = it->second.second;
+    live_.erase(it);
+    if (!events_.empty()) {
+      b.ready = events_.back();
+      events_.pop_back();
+    } else if (hipEventCreateWithFlags(&b.ready, hipEventDisableTiming) != hipSuccess) {
+      b.ready = nullptr;
+    }
+    if (b.ready == nullptr || hipEventRecord(b.ready, s) != hipSuccess) {
+      // no event: drain the stream so the block is idle
+      (void)hipStreamSynchronize(s);
+      if (b.ready == nullptr) (void)hipEventCreateWithFlags(&b.ready, hipEventDisableTiming);
+    }
+    free_.emplace(std::make_pair(dev, b.size), b);
+    cached_ += b.size;
+  }
+
+  // Returns idle cached blocks to the device (allocation failure path).
+  void Release() {
+    std::lock_guard<std::mutex> l(mu_);
+    for (auto it = free_.begin(); it != free_.end();) {
+      Block& b = it->second;
+      if (b.ready) (void)hipEventSynchronize(b.ready);
+      (void)hipFree(b.p);
+      if (b.ready) events_.push_back(b.ready);
+      cached_ -= b.size;
+      it = free_.erase(it);
+    }
+  }
+
+ private:
+  struct Block {
+    void* p;
+    size_t size;
+    hipStream_t stream;
+    hipEvent_t ready;
+  };
+  static size_t Bucket(size_t n) {
+    if (n <= (size_t{1} << 20)) {
+      size_t b = 512;
+      while (b < n) b <<= 1;
+      return b;
+    }
+    const size_t g = size_t{2} << 20;
+    return (n + g - 1) / g * g;
+  }
+  std::mutex mu_;
+  std::unordered_map<void*, std::pair<size_t, int>> live_;  // block -> (size, device)
+  std::multimap<std::pair<int, size_t>, Block> free_;        // (device, size) -> idle block
+  std::vector<hipEvent_t> events_;                           // recycled
+  size_t cached_ = 0;
+};
+
+// DPF_AMD_DEBUG_ALLOC=1: every live DeviceBuffer range is registered and a
+// new allocation overlapping a live one is reported on stderr (diagnostics
+// for the stream-ordered pool).
+struct LiveRanges {
+  std::mutex mu;
+  std::map<uintptr_t, size_t> live;
+  static LiveRanges& Get() {
+    static LiveRanges r;
+    return r;
+  }
+  static bool On() {
+    static const bool on = std::getenv("DPF_AMD_DEBUG_ALLOC") != nullptr;
+    return on;
+  }
+  void Add(void* p, size_t n) {
+    std::lock_guard<std::mutex> l(mu);
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    auto it = live.upper_bound(a);
+    if (it != live.end() && it->first < a + n)
+      std::fprintf(stderr, "[dpf_amd] alloc %p+%zu overlaps live %p+%zu\n", p, n,
+                   reinterpret_cast<void*>(it->first), it->second);
+    if (it != live.begin()) {
+      --it;
+      if (it->first + it->second > a)
+        std::fprintf(stderr, "[dpf_amd] alloc %p+%zu overlaps live %p+%zu\n", p, n,
+                     reinterpret_cast<void*>(it->first), it->second);
+    }
+    live[a] = n;
+  }
+  void Remove(void* p) {
+    std::lock_guard<std::mutex> l(mu);
+    live.erase(reinterpret_cast<uintptr_t>(p));
+  }
+};
+
 class DeviceBuffer {
  public:
   DeviceBuffer() = default;
@@ -92,18 +334,35 @@ class DeviceBuffer {
     Reset();
     stream_ = s;
     if (bytes == 0) bytes = 16;
-    return HipStatus(hipMallocAsync(&p_, bytes, s), "hipMallocAsync");
+    Status st = NoPool() ? HipStatus(hipMalloc(&p_, bytes), "hipMalloc")
+                         : DevicePool::Get().Alloc(bytes, s, &p_);
+    if (st.ok() && LiveRanges::On()) LiveRanges::Get().Add(p_, bytes);
+    return st;
   }
   Status Upload(const void* src, size_t bytes, hipStream_t s) {
     DPF_RETURN_IF_ERROR(Alloc(bytes, s));
     if (bytes == 0) return OkStatus();
-    return HipStatus(hipMemcpyAsync(p_, src, bytes, hipMemcpyHostToDevice, s), "upload");
+    return ThreadUploadRing().Copy(p_, src, bytes, s);
   }
   void Reset() {
-    if (p_) (void)hipFreeAsync(p_, stream_);
+    if (p_) {
+      if (LiveRanges::On()) LiveRanges::Get().Remove(p_);
+      if (NoPool()) {
+        (void)hipStreamSynchronize(stream_);
+        (void)hipFree(p_);
+      } else {
+        DevicePool::Get().Free(p_, stream_);
+      }
+    }
     p_ = nullptr;
   }
   void* get() const { return p_; }
+  // DPF_AMD_NO_POOL=1 (diagnostics): synchronous hipMalloc / hipFree instead
+  // of the caching pool.
+  static bool NoPool() {
+    static const bool on = std::getenv("DPF_AMD_NO_POOL") != nullptr;
+    return on;
+  }
   template <typename T>
   T* as() const {
     return static_cast<T*>(p_);

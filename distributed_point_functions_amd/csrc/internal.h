@@ -45,6 +45,11 @@ struct alignas(16) VtDev {
   u128 corr_packed;  // single-scalar direct types: corrections packed like a block
 };
 
+// Stream-ordered copy of `bytes` from host memory mapped into the device
+// address space (hipHostMalloc) to device memory, done by a kernel on
+// `stream` (host_device.h UploadRing).
+int CopyFromMappedHost(void* dst, const void* mapped_src, size_t bytes, void* stream);
+
 // Fills the device descriptor; returns a status code.
 int MakeVtDev(const dpf_amd_value_type& vt, const uint64_t* correction,
               int party, int cepb, VtDev* out);

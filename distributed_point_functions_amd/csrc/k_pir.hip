@@ -27,26 +27,39 @@ __device__ __forceinline__ uint4 LoadRecordWord(const uint4* p) {
 // Gather / fold helpers
 // ----------------------------------------------------------------------------
 
+// Source rows outside [0, in_rows - opp] are not read: the segment is
+// skipped and *err set (callers that know the source size pass it; the C ABI
+// entry passes INT64_MAX and no flag).
+__device__ __forceinline__ bool GatherRowOk(int64_t r, int64_t opp, int64_t in_rows, int* err) {
+  if (r >= 0 && r <= in_rows - opp) return true;
+  if (err) *err = 1;
+  return false;
+}
+
 __global__ void KGatherRows(int64_t n, const int64_t* src_offset, int64_t opp,
-                            int64_t stride, const char* in, char* out) {
+                            int64_t stride, const char* in, char* out, int64_t in_rows,
+                            int* err) {
   const int64_t total = n * opp * stride;
   const int64_t step = (int64_t)gridDim.x * blockDim.x;
   for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < total; b += step) {
     const int64_t row = b / stride, byte = b % stride;
     const int64_t i = row / opp, k = row % opp;
-    out[b] = in[(src_offset[i] + k) * stride + byte];
+    const int64_t r = src_offset[i];
+    if (GatherRowOk(r, opp, in_rows, err)) out[b] = in[(r + k) * stride + byte];
   }
 }
 
 // 16-byte variant: every segment (opp x stride bytes) is a whole number of
 // 16-byte words at a 16-byte-aligned source offset.
 __global__ void KGatherRows16(int64_t n, const int64_t* src_offset, int64_t seg_words,
-                              int64_t src_words_per_unit, const uint4* in, uint4* out) {
+                              int64_t src_words_per_unit, const uint4* in, uint4* out,
+                              int64_t opp, int64_t in_rows, int* err) {
   const int64_t total = n * seg_words;
   const int64_t step = (int64_t)gridDim.x * blockDim.x;
   for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total; w += step) {
     const int64_t i = w / seg_words, k = w - i * seg_words;
-    out[w] = in[src_offset[i] * src_words_per_unit + k];
+    const int64_t r = src_offset[i];
+    if (GatherRowOk(r, opp, in_rows, err)) out[w] = in[r * src_words_per_unit + k];
   }
 }
 
@@ -55,12 +68,14 @@ __global__ void KGatherRows16(int64_t n, const int64_t* src_offset, int64_t seg_
 // rows_per_word (EvaluateUntil's offsets are multiples of opp); other
 // segments are copied byte-wise.
 __global__ void KGatherRowsSmall(int64_t n, const int64_t* src_offset, int64_t seg_words,
-                                 int64_t rows_per_word, const uint4* in, uint4* out) {
+                                 int64_t rows_per_word, const uint4* in, uint4* out,
+                                 int64_t opp, int64_t in_rows, int* err) {
   const int64_t total = n * seg_words;
   const int64_t step = (int64_t)gridDim.x * blockDim.x;
   for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total; w += step) {
     const int64_t i = w / seg_words, k = w - i * seg_words;
     const int64_t r = src_offset[i];
+    if (!GatherRowOk(r, opp, in_rows, err)) continue;
     if (r % rows_per_word == 0) {
       out[w] = in[r / rows_per_word + k];
     } else {
@@ -69,6 +84,29 @@ __global__ void KGatherRowsSmall(int64_t n, const int64_t* src_offset, int64_t s
       for (int b = 0; b < 16; ++b) dst[b] = src[b];
     }
   }
+}
+
+// Host-to-device upload as a kernel on the caller's stream: 16-byte words
+// (the tail byte-wise) read from pinned host memory mapped into the device
+// address space.
+__global__ void KCopyFromHost(char* dst, const char* src, int64_t bytes) {
+  const int64_t words = bytes / 16;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  const int64_t first = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t w = first; w < words; w += step)
+    reinterpret_cast<uint4*>(dst)[w] = reinterpret_cast<const uint4*>(src)[w];
+  for (int64_t b = words * 16 + first; b < bytes; b += step) dst[b] = src[b];
+}
+
+int CopyFromMappedHost(void* dst, const void* mapped_src, size_t bytes, void* stream) {
+  if (bytes == 0) return DPF_AMD_OK;
+  if ((uintptr_t)dst % 16 || (uintptr_t)mapped_src % 16)
+    return SetError(DPF_AMD_INTERNAL, "upload buffers must be 16-byte aligned");
+  const int64_t words = (int64_t)(bytes + 15) / 16;
+  const int grid = (int)std::min<int64_t>(1024, (words + 255) / 256);
+  hipLaunchKernelGGL(KCopyFromHost, dim3(grid), dim3(256), 0, (hipStream_t)stream, (char*)dst,
+                     (const char*)mapped_src, (int64_t)bytes);
+  return LaunchCheck("upload kernel launch");
 }
 
 // XOR of num_parts equally sized partial vectors.  A 256-thread block owns
@@ -268,20 +306,23 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
 }
 
 int LaunchGatherRows(int grid, hipStream_t st, int64_t n, const int64_t* src_offset,
-                     int64_t opp, int64_t stride, const char* in, char* out) {
+                     int64_t opp, int64_t stride, const char* in, char* out, int64_t in_rows,
+                     int* err) {
   // Row offsets are multiples of opp rows; with (opp x stride) % 16 == 0 and
   // 16-byte-aligned buffers every segment is whole 16-byte words.
   if ((opp * stride) % 16 == 0 && (uintptr_t)in % 16 == 0 && (uintptr_t)out % 16 == 0 &&
       (opp * stride) / 16 > 0 && stride % 16 == 0) {
     hipLaunchKernelGGL(KGatherRows16, dim3(grid), dim3(256), 0, st, n, src_offset,
-                       opp * stride / 16, stride / 16, (const uint4*)in, (uint4*)out);
+                       opp * stride / 16, stride / 16, (const uint4*)in, (uint4*)out, opp,
+                       in_rows, err);
   } else if ((opp * stride) % 16 == 0 && (uintptr_t)in % 16 == 0 && (uintptr_t)out % 16 == 0 &&
              (16 % stride) == 0) {
     hipLaunchKernelGGL(KGatherRowsSmall, dim3(grid), dim3(256), 0, st, n, src_offset,
-                       opp * stride / 16, 16 / stride, (const uint4*)in, (uint4*)out);
+                       opp * stride / 16, 16 / stride, (const uint4*)in, (uint4*)out, opp,
+                       in_rows, err);
   } else {
     hipLaunchKernelGGL(KGatherRows, dim3(grid), dim3(256), 0, st, n, src_offset, opp, stride,
-                       in, out);
+                       in, out, in_rows, err);
   }
   return LaunchCheck("gather kernel launch");
 }

@@ -381,6 +381,16 @@ int dpf_amd_gather_rows(int64_t num_prefixes, const int64_t* src_offset,
                           src_offset, outputs_per_prefix, stride, (const char*)in, (char*)out);
 }
 
+int dpf_amd_gather_rows_checked(int64_t num_prefixes, const int64_t* src_offset,
+                                int64_t outputs_per_prefix, int64_t stride, const void* in,
+                                int64_t in_rows, void* out, int* err, void* stream) {
+  if (num_prefixes <= 0 || outputs_per_prefix <= 0) return DPF_AMD_OK;
+  const int64_t total = num_prefixes * outputs_per_prefix * stride;
+  return LaunchGatherRows(GridFor(total, 256, 8192), (hipStream_t)stream, num_prefixes,
+                          src_offset, outputs_per_prefix, stride, (const char*)in, (char*)out,
+                          in_rows, err);
+}
+
 int dpf_amd_xor_fold(const void* parts, int num_parts, int64_t bytes, void* out,
                      void* stream) {
   if (num_parts <= 0 || bytes <= 0) return DPF_AMD_OK;

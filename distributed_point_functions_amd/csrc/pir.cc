@@ -8,6 +8,7 @@
 
 #include "dpf_amd/dense_dpf_pir_server.h"
 #include "host_aes.h"
+#include "host_device.h"
 #include "internal.h"
 
 namespace distributed_point_functions {
@@ -149,16 +150,16 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductWithDevice(
   const int64_t ws = dpf_amd_inner_product_workspace_size(num_records_, stride_, num_queries);
   void* work = nullptr;
   void* out = nullptr;
-  DPF_RETURN_IF_ERROR(HipStatus(hipMallocAsync(&work, std::max<int64_t>(ws, 16), s), "alloc"));
-  Status st = HipStatus(hipMallocAsync(&out, num_queries * stride_, s), "alloc");
+  DPF_RETURN_IF_ERROR(dpf_internal_host::DevicePool::Get().Alloc(std::max<int64_t>(ws, 16), s, &work));
+  Status st = dpf_internal_host::DevicePool::Get().Alloc(num_queries * stride_, s, &out);
   std::vector<char> host(num_queries * stride_);
   if (st.ok())
     st = AbiStatus(dpf_amd_inner_product(records_, num_records_, stride_, selections_dev,
                                          selection_blocks, num_queries, work, out, s));
   if (st.ok())
     st = HipStatus(hipMemcpyAsync(host.data(), out, host.size(), hipMemcpyDeviceToHost, s), "d2h");
-  (void)hipFreeAsync(work, s);
-  if (out) (void)hipFreeAsync(out, s);
+  dpf_internal_host::DevicePool::Get().Free(work, s);
+  if (out) dpf_internal_host::DevicePool::Get().Free(out, s);
   Status sync = HipStatus(hipStreamSynchronize(s), "sync");
   if (!st.ok()) return st;
   if (!sync.ok()) return sync;
@@ -194,12 +195,12 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductWith(
       host[k * blocks + b] = selections[k][b].value();
   hipStream_t s = PirStream();
   void* dev = nullptr;
-  DPF_RETURN_IF_ERROR(HipStatus(hipMallocAsync(&dev, 16 * host.size(), s), "alloc"));
+  DPF_RETURN_IF_ERROR(dpf_internal_host::DevicePool::Get().Alloc(16 * host.size(), s, &dev));
   Status st = HipStatus(hipMemcpyAsync(dev, host.data(), 16 * host.size(),
                                        hipMemcpyHostToDevice, s), "h2d");
   StatusOr<std::vector<std::string>> r =
       st.ok() ? InnerProductWithDevice(dev, blocks, q, s) : StatusOr<std::vector<std::string>>(st);
-  (void)hipFreeAsync(dev, s);
+  dpf_internal_host::DevicePool::Get().Free(dev, s);
   (void)hipStreamSynchronize(s);
   return r;
 }
@@ -380,7 +381,7 @@ StatusOr<PirResponse> DenseDpfPirServer::HandlePlainRequest(const PirRequest& re
     const int64_t blocks = std::max<int64_t>(1, (n + 127) / 128);
     hipStream_t s = PirStream();
     void* sel = nullptr;
-    DPF_RETURN_IF_ERROR(HipStatus(hipMallocAsync(&sel, 16 * blocks * q, s), "alloc"));
+    DPF_RETURN_IF_ERROR(dpf_internal_host::DevicePool::Get().Alloc(16 * blocks * q, s, &sel));
     const dpf_amd_value_type layout = dpf_internal::HostLayoutOf<XorWrapper<uint128>>();
     std::vector<const DpfKey*> keys(q);
     for (int i = 0; i < q; ++i) keys[i] = &plain.dpf_key(i);
@@ -389,7 +390,7 @@ StatusOr<PirResponse> DenseDpfPirServer::HandlePlainRequest(const PirRequest& re
     StatusOr<std::vector<std::string>> r =
         st.ok() ? gpu_db->InnerProductWithDevice(sel, blocks, q, s)
                 : StatusOr<std::vector<std::string>>(st);
-    (void)hipFreeAsync(sel, s);
+    dpf_internal_host::DevicePool::Get().Free(sel, s);
     (void)hipStreamSynchronize(s);
     if (!r.ok()) return r.status();
     inner_products = std::move(*r);

@@ -204,6 +204,14 @@ int dpf_amd_gather_rows(int64_t num_prefixes, const int64_t* src_offset,
                         int64_t outputs_per_prefix, int64_t stride,
                         const void* in, void* out, void* stream);
 
+/* As dpf_amd_gather_rows with the source size: segments whose source rows
+ * fall outside [0, in_rows) are skipped and *err (device int, may be NULL)
+ * is set to 1 instead of reading out of bounds. */
+int dpf_amd_gather_rows_checked(int64_t num_prefixes, const int64_t* src_offset,
+                                int64_t outputs_per_prefix, int64_t stride,
+                                const void* in, int64_t in_rows, void* out, int* err,
+                                void* stream);
+
 /* Replaces pir_internal::InnerProduct (pir/internal/inner_product_hwy.h:
  * 38-41) for a database stored with a fixed, 16-byte-aligned record stride:
  * for query q, out[q] = XOR of records r < num_records whose selection bit

@@ -8,6 +8,7 @@
 //   distributed_comparison_function_test.cc:106-133 (GenEval).
 // Exit status 0 = all checks passed.  Built and run by tests/test_cpp_api.py.
 #include <cstdio>
+#include <set>
 #include <vector>
 
 #include "dpf_amd/distributed_comparison_function.h"
@@ -188,9 +189,64 @@ static int EvaluateAndApplyStops() {
   return 0;
 }
 
+// Incremental evaluation with many surviving prefixes per level (the c3
+// heavy-hitters shape, smaller): share sums at every level.  Run under the
+// ROCm runtime in /opt/rocm (not torch's), this is the case that exposed the
+// hipMallocAsync pool issue host_device.h's DevicePool works around.
+static int IncrementalManyPrefixes() {
+  const int H = 8;
+  std::vector<DpfParameters> ps(H);
+  for (int i = 0; i < H; ++i) {
+    ps[i].set_log_domain_size(8 * (i + 1));
+    ps[i].mutable_value_type()->mutable_integer()->set_bitsize(64);
+  }
+  auto dpf = DistributedPointFunction::CreateIncremental(ps);
+  CHECK_OK(dpf);
+  const uint128 alpha = 0x0123456789abcdefull;
+  std::vector<uint128> betas(H);
+  for (int i = 0; i < H; ++i) betas[i] = 1000 + i;
+  auto keys = (*dpf)->GenerateKeysIncremental(alpha, betas);
+  CHECK_OK(keys);
+  auto c0 = (*dpf)->CreateEvaluationContext(keys->first);
+  auto c1 = (*dpf)->CreateEvaluationContext(keys->second);
+  CHECK_OK(c0);
+  CHECK_OK(c1);
+  std::vector<uint128> prefixes;
+  uint64_t x = 88172645463325252ull;  // xorshift64
+  for (int i = 0; i < H; ++i) {
+    auto a = (*dpf)->EvaluateNext<uint64_t>(prefixes, *c0);
+    auto b = (*dpf)->EvaluateNext<uint64_t>(prefixes, *c1);
+    CHECK_OK(a);
+    CHECK_OK(b);
+    size_t nonzero = 0;
+    for (size_t j = 0; j < a->size(); ++j) {
+      const uint64_t s = (*a)[j] + (*b)[j];
+      if (s) {
+        ++nonzero;
+        CHECK(s == 1000u + i);
+      }
+    }
+    CHECK(nonzero == 1);
+    if (i + 1 == H) break;
+    // next level's candidates: 2^14 distinct children of these prefixes,
+    // alpha's included
+    std::set<uint128> next;
+    next.insert(alpha >> (64 - 8 * (i + 1)));
+    while (next.size() < (i == 0 ? size_t{256} : size_t{1} << 14)) {
+      x ^= x << 13;
+      x ^= x >> 7;
+      x ^= x << 17;
+      const uint128 parent = prefixes.empty() ? 0 : prefixes[x % prefixes.size()];
+      next.insert(prefixes.empty() ? uint128(x & 255) : (parent << 8) | ((x >> 32) & 255));
+    }
+    prefixes.assign(next.begin(), next.end());
+  }
+  return 0;
+}
+
 int main() {
   if (FullDomainUint64() || IncrementalTuple() || DcfGenEval() || Registration() ||
-      EvaluateAndApplyStops())
+      EvaluateAndApplyStops() || IncrementalManyPrefixes())
     return 2;
   if (failures) {
     std::fprintf(stderr, "%d check(s) failed\n", failures);

@@ -145,6 +145,27 @@ void C3(int reps) {
     }
     prefixes[i].assign(cur.begin(), cur.end());
   }
+  if (const char* dump = std::getenv("DPF_AMD_BENCH_DUMP")) {
+    // keys + prefixes, for replaying this case elsewhere (tools/replay_c3.py)
+    FILE* f = std::fopen(dump, "wb");
+    if (f) {
+      for (const DpfKey* k : {&keys->first, &keys->second}) {
+        const std::string b = k->SerializeAsString();
+        const uint64_t n = b.size();
+        std::fwrite(&n, 8, 1, f);
+        std::fwrite(b.data(), 1, n, f);
+      }
+      const uint64_t a[2] = {static_cast<uint64_t>(alpha), static_cast<uint64_t>(alpha >> 64)};
+      std::fwrite(a, 8, 2, f);
+      for (int i = 0; i < H; ++i) {
+        const uint64_t b = static_cast<uint64_t>(betas[i]), n = prefixes[i].size();
+        std::fwrite(&b, 8, 1, f);
+        std::fwrite(&n, 8, 1, f);
+        std::fwrite(prefixes[i].data(), 16, n, f);
+      }
+      std::fclose(f);
+    }
+  }
   std::vector<double> best(H, 1e30);
   double best_total = 1e30;
   size_t leaves = 0;
@@ -172,9 +193,16 @@ void C3(int reps) {
           const uint64_t s = (*a)[x] + (*b)[x];
           if (s != 0) {
             ++nonzero;
+            if (s != static_cast<uint64_t>(betas[i]) && ok)
+              std::fprintf(stderr, "c3 level %d: share sum %llu at %zu, beta %llu\n", i,
+                           static_cast<unsigned long long>(s), x,
+                           static_cast<unsigned long long>(betas[i]));
             ok &= s == static_cast<uint64_t>(betas[i]);
           }
         }
+        if (nonzero != 1 && ok)
+          std::fprintf(stderr, "c3 level %d: %zu non-zero share sums of %zu\n", i, nonzero,
+                       a->size());
         ok &= nonzero == 1;
       }
     }
