@@ -8,6 +8,7 @@ from __future__ import annotations
 import concurrent.futures
 import glob
 import os
+import re
 import subprocess
 import sys
 
@@ -43,10 +44,33 @@ def _headers_mtime():
     return max([os.path.getmtime(h) for h in hs] + [0])
 
 
+_INCLUDE_RE = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _deps_mtime(src: str) -> float:
+    """Newest mtime of `src` and the project headers it includes (quoted
+    includes, followed recursively through csrc/ and include/)."""
+    seen, todo, newest = set(), [src], 0.0
+    while todo:
+        f = todo.pop()
+        if f in seen:
+            continue
+        seen.add(f)
+        newest = max(newest, os.path.getmtime(f))
+        with open(f, errors="replace") as fh:
+            text = fh.read()
+        for inc in _INCLUDE_RE.findall(text):
+            for d in (os.path.dirname(f), CSRC, os.path.join(ROOT, "include")):
+                cand = os.path.join(d, inc)
+                if os.path.exists(cand):
+                    todo.append(os.path.normpath(cand))
+                    break
+    return newest
+
+
 def _compile(src: str, force: bool, obj_dir: str = OBJ_DIR, defines=()) -> str:
     obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
-    if (not force and os.path.exists(obj) and
-            os.path.getmtime(obj) >= max(os.path.getmtime(src), _headers_mtime())):
+    if not force and os.path.exists(obj) and os.path.getmtime(obj) >= _deps_mtime(src):
         return obj
     cmd = ["hipcc"] + CXXFLAGS + ["-D" + d for d in defines] + ["-c", src, "-o", obj + ".tmp"]
     if src.endswith(".hip"):

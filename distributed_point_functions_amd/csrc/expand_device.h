@@ -15,11 +15,29 @@
 #define DPF_EXPAND_MAX_GRID (1 << 24)
 #endif
 
+// Leaves a lane keeps in registers before storing them as one contiguous
+// burst (0: every leaf is stored as it is produced).  A lane's leaves are
+// consecutive in the output, so 8 x 16 B fill a whole 128-byte line at once
+// instead of leaving it partly written in L2 across 8 leaves of compute.
+// The 32 staging VGPRs need the 4-wave/SIMD register budget, so the staged
+// emitters launch 512-thread blocks (2 per CU, one 64 KiB table each).
+// Measured on MI355X, c5 KExpand<8, EmitU32ModN64>: 178.8 ms unstaged at 6
+// waves/SIMD (19 VGPRs spilled to scratch), 181.2 ms unstaged at 4, 164.6 ms
+// staged at 4 (no spills), 171.3 ms staged at 5.
+#ifndef DPF_STAGE_LEAVES
+#define DPF_STAGE_LEAVES 8
+#endif
+#ifndef DPF_STAGED_BLOCK
+#define DPF_STAGED_BLOCK 512
+#define DPF_STAGED_WAVES 4
+#endif
+
 namespace dpf_amd {
 
 template <int BN>
 struct EmitGeneric {
   static constexpr int kBN = BN;
+  static constexpr bool kCanStage = false;
   __device__ static void Emit(const ExpandCtx& E, const uint32_t (&h)[BN][4], uint32_t t,
                               int64_t g) {
     const VtDev& vt = E.vt;
@@ -100,6 +118,7 @@ __device__ __forceinline__ void StoreLeaf16(const ExpandCtx& E, const uint4& v, 
 template <int B>
 struct EmitDirect {
   static constexpr int kBN = 1;
+  static constexpr bool kCanStage = true;  // when Packed(vt)
   // Whole 16-byte blocks per leaf (every element of the block is returned).
   __device__ static bool Packed(const VtDev& vt) { return vt.cepb * B == 16; }
   __device__ static uint4 Value(const ExpandCtx& E, const uint32_t (&h)[1][4], uint32_t t) {
@@ -142,6 +161,7 @@ struct EmitDirect {
 // bytes[16..20); element 1 = block mod m.
 struct EmitU32ModN64 {
   static constexpr int kBN = 2;
+  static constexpr bool kCanStage = true;  // when Packed(vt)
   // libstdc++ tuple layout: u64 at 0, u32 at 8, stride 16.
   __device__ static bool Packed(const VtDev& vt) {
     return vt.sc[0].out_off == 8 && vt.sc[1].out_off == 0 && vt.stride == 16;
@@ -205,16 +225,61 @@ struct EmitU32ModN64 {
 // (chunk << D) + j.
 // ----------------------------------------------------------------------------
 
+template <class Em>
+constexpr bool kStagedEm = DPF_STAGE_LEAVES > 0 && Em::kCanStage;
+template <class Em>
+constexpr int kBlockOf = kStagedEm<Em> ? DPF_STAGED_BLOCK : kExpandBlock;
+template <class Em>
+constexpr int kWavesOf = kStagedEm<Em> ? DPF_STAGED_WAVES : kExpandWaves;
+
+struct LeafStage {
+  uint4 v[DPF_STAGE_LEAVES > 0 ? DPF_STAGE_LEAVES : 1];
+};
+
+template <class Em, int D>
+constexpr bool kStaged = kStagedEm<Em> && (1 << D) >= DPF_STAGE_LEAVES;
+
+// Leaf j of the lane's subtree (j wave-uniform): staged when the emitter
+// writes packed 16-byte leaves, flushed as one burst per DPF_STAGE_LEAVES.
+template <int D, class Em, int BN>
+__device__ __forceinline__ void EmitStagedLeaf(const ExpandCtx& E, LeafStage& S,
+                                         const uint32_t (&h)[BN][4], uint32_t t,
+                                         int64_t chunk, int j) {
+  if constexpr (kStaged<Em, D>) {
+    if (Em::Packed(E.vt)) {
+      constexpr int N = DPF_STAGE_LEAVES;
+      const uint4 v = Em::Value(E, h, t);
+      const int k = j & (N - 1);
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        if (i == k) S.v[i] = v;
+      if (k == N - 1) {
+        const int64_t g0 = (chunk << D) + j - (N - 1);
+        if (g0 >= E.a.leaf_begin && g0 + N <= E.a.leaf_end) {
+          uint4* dst = reinterpret_cast<uint4*>(E.a.out) + (g0 - E.a.leaf_begin);
+#pragma unroll
+          for (int i = 0; i < N; ++i) dst[i] = S.v[i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < N; ++i) StoreLeaf16(E, S.v[i], g0 + i);
+        }
+      }
+      return;
+    }
+  }
+  Em::Emit(E, h, t, (chunk << D) + j);
+}
+
 template <int DEPTH, int D, class Em>
-__device__ __forceinline__ void Dfs(const ExpandCtx& E, const uint32_t (&x)[4], uint32_t t,
-                                    int level, int64_t chunk, int j) {
+__device__ __forceinline__ void Dfs(const ExpandCtx& E, LeafStage& S, const uint32_t (&x)[4],
+                                    uint32_t t, int level, int64_t chunk, int j) {
   constexpr int BN = Em::kBN;
   if constexpr (DEPTH == 0) {
     uint32_t xs[1][4] = {{x[0], x[1], x[2], x[3]}};
     uint32_t h[1][BN][4];
     // For D > 0 the seed comes out of Expand2 with its LSB cleared.
     HashWords<1, BN, (D > 0)>(xs, h, E.L);
-    Em::Emit(E, h[0], t, (chunk << D) + j);
+    EmitStagedLeaf<D, Em, BN>(E, S, h[0], t, chunk, j);
   } else {
     const Cw cw = LoadCw(E.a.cw_seed, E.a.ccl, E.a.ccr, level);
     uint32_t l[4], r[4], tl, tr;
@@ -223,8 +288,8 @@ __device__ __forceinline__ void Dfs(const ExpandCtx& E, const uint32_t (&x)[4], 
       uint32_t xs[2][4] = {{l[0], l[1], l[2], l[3]}, {r[0], r[1], r[2], r[3]}};
       uint32_t h[2][1][4];
       HashWords<2, 1>(xs, h, E.L);
-      Em::Emit(E, h[0], tl, (chunk << D) + 2 * j);
-      Em::Emit(E, h[1], tr, (chunk << D) + 2 * j + 1);
+      EmitStagedLeaf<D, Em, 1>(E, S, h[0], tl, chunk, 2 * j);
+      EmitStagedLeaf<D, Em, 1>(E, S, h[1], tr, chunk, 2 * j + 1);
     } else {
       // Only the right child stays live across the left recursion (its
       // control bit packed into its seed's LSB); the left child is consumed
@@ -234,7 +299,7 @@ __device__ __forceinline__ void Dfs(const ExpandCtx& E, const uint32_t (&x)[4], 
       uint32_t ty = tl;
 #pragma unroll 1
       for (int b = 0; b < 2; ++b) {
-        Dfs<DEPTH - 1, D, Em>(E, y, ty, level + 1, chunk, 2 * j + b);
+        Dfs<DEPTH - 1, D, Em>(E, S, y, ty, level + 1, chunk, 2 * j + b);
 #pragma unroll
         for (int c = 0; c < 4; ++c) y[c] = r[c];
         ty = y[0] & 1u;
@@ -245,7 +310,7 @@ __device__ __forceinline__ void Dfs(const ExpandCtx& E, const uint32_t (&x)[4], 
 }
 
 template <int D, class Em>
-__global__ __launch_bounds__(kExpandBlock, kExpandWaves) void KExpand(ExpandArgs a, VtDev vt) {
+__global__ __launch_bounds__(kBlockOf<Em>, kWavesOf<Em>) void KExpand(ExpandArgs a, VtDev vt) {
   __shared__ uint32_t tab[kTabWords];
   FillTables(tab);
   __syncthreads();
@@ -285,18 +350,22 @@ __global__ __launch_bounds__(kExpandBlock, kExpandWaves) void KExpand(ExpandArgs
         t = bit ? tr : tl;
       }
     }
-    if (live) Dfs<D, D, Em>(E, x, t, a.walk, c, 0);
+    LeafStage S;
+    if (live) Dfs<D, D, Em>(E, S, x, t, a.walk, c, 0);
   }
 }
 
 template <int D, class Em>
-int LaunchExpand(int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
+int LaunchExpand(int, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
   // One subtree per thread, many more blocks than resident slots: blocks
   // finish at different times (per-CU clocks differ) and the dispatcher
   // back-fills.  c5: 2^24 subtrees / 768 = 21845 blocks -> 166.8 ms, vs
   // 173.8 ms capped at 2730 blocks and 180.5 ms at one resident round.
-  grid = std::min(grid, DPF_EXPAND_MAX_GRID);
-  hipLaunchKernelGGL((KExpand<D, Em>), dim3(grid), dim3(kExpandBlock), 0, st, a, vt);
+  constexpr int block = kBlockOf<Em>;
+  const int64_t chunks = a.chunk_end - a.chunk_begin;
+  const int grid = (int)std::max<int64_t>(
+      1, std::min<int64_t>((chunks + block - 1) / block, DPF_EXPAND_MAX_GRID));
+  hipLaunchKernelGGL((KExpand<D, Em>), dim3(grid), dim3(block), 0, st, a, vt);
   return LaunchCheck("expand kernel launch");
 }
 

@@ -45,7 +45,7 @@ inline hipStream_t ThreadStream() {
       if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
     }
     ~Holder() {
-      if (s) hipStreamDestroy(s);
+      if (s) (void)hipStreamDestroy(s);
     }
   };
   thread_local Holder h;
@@ -207,7 +207,12 @@ class DevicePool {
       auto range = free_.equal_range(std::make_pair(dev, size));
       for (auto it = range.first; it != range.second; ++it) {
         Block& b = it->second;
-        if (b.stream != s && hipEventQuery(b.ready) != hipSuccess) continue;
+        if (b.stream != s && hipEventQuery(b.ready) != hipSuccess) {
+          // not-ready is the expected answer; clear it so the next launch
+          // check (hipGetLastError) does not report it as its own failure
+          (void)hipGetLastError();
+          continue;
+        }
         *out = b.p;
         events_.push_back(b.ready);
         live_[b.p] = std::make_pair(size, dev);
@@ -246,6 +251,7 @@ class DevicePool {
     }
     if (b.ready == nullptr || hipEventRecord(b.ready, s) != hipSuccess) {
       // no event: drain the stream so the block is idle
+      (void)hipGetLastError();
       (void)hipStreamSynchronize(s);
       if (b.ready == nullptr) (void)hipEventCreateWithFlags(&b.ready, hipEventDisableTiming);
     }

@@ -305,6 +305,150 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
   FoldPartials<QN>(a, acc, red, Cs, G, active, chunk_lo);
 }
 
+// ----------------------------------------------------------------------------
+// Many-query scan: method of Four Russians over 4-record groups
+// ----------------------------------------------------------------------------
+//
+// The masked scan spends one VALU op per (query, record dword); at Q = 64 that
+// is VALU-issue bound far above the HBM floor.  Here a wave reads a 256-byte
+// column slice of 4 consecutive records (lane j = dword j, one coalesced
+// load per record), builds the 16 XOR combinations of the 4 slices once in
+// LDS (11 XORs, 15 row stores), and every query then costs ONE table row
+// read — the row its 4 selection bits index — and the XORs of that row into
+// its accumulators.  Lanes are (query, column part): 64 / P queries per wave,
+// each lane owning 256 / P bytes of the slice as P-th of the row, read with
+// ds_read_b128.  Table rows are 272 B apart, so the 16-byte slot of row e,
+// column c is (e + c) mod 16: lanes of a ds_read_b128 group that read
+// different rows hit different slots and lanes reading the same row
+// broadcast — conflict-free for any selection.  Each wave owns its table (no
+// block barrier); its accumulators are one partial of the fold
+// (part = blockIdx.x * kScanM4Waves + wave, parts < a.parts).
+//
+// LDS traffic per 4 records: 15 row stores (64 lanes x 4 B) + QW rows read
+// (256 B each); VALU: 11 + 2 + 64 XORs per lane.  Records past num_records
+// and slice dwords past the record read as zero, so they add nothing.
+// One 128-record tile.  FULL tiles read the records through a buffer
+// resource based at the tile (record offsets in SGPRs, nontemporal); the
+// last, partial tile reads records past num_records as zero.
+template <int P, bool FULL>
+__device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint4 s,
+                                           uint32_t (&acc)[64 / P], uint32_t* t, int lane,
+                                           int cpart, bool col_ok, int dw_lo) {
+  constexpr int CPL = 16 / P;
+  constexpr int ROW = 17;
+  const int rec_dwords = a.C * 4;
+  const int64_t rec0 = tile << 7;
+  const uint32_t* base = reinterpret_cast<const uint32_t*>(a.db) + rec0 * rec_dwords + dw_lo;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+  // lanes past the slice's width read beyond num_records (0x7fffffff): zero.
+  // Record offsets go in soffset (< 128 * rec_bytes <= 2^27, see ScanM4Parts).
+  const int voff = col_ok ? lane * 4 : (int)0x80000000u;
+  auto load = [&](int r) -> uint32_t {
+    if constexpr (FULL) {
+      return __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, r * rec_dwords * 4, 2);
+    } else {
+      return (col_ok && rec0 + r < a.num_records) ? base[(int64_t)r * rec_dwords + lane] : 0u;
+    }
+  };
+  uint32_t xn[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) xn[i] = load(i);
+#pragma unroll 1
+  for (int k = 0; k < 32; ++k) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t x[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = xn[i];
+    // next group (the last group re-reads the tile's first, cached, records
+    // rather than branching)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xn[i] = load((4 * (k + 1) + i) & 127);
+    const uint32_t x01 = x[0] ^ x[1], x012 = x01 ^ x[2];
+    const uint32_t r[16] = {0u,          x[0],        x[1],        x01,
+                            x[2],        x[0] ^ x[2], x[1] ^ x[2], x012,
+                            x[3],        x[0] ^ x[3], x[1] ^ x[3], x01 ^ x[3],
+                            x[2] ^ x[3], x[0] ^ x[2] ^ x[3], x[1] ^ x[2] ^ x[3], x012 ^ x[3]};
+#pragma unroll
+    for (int e = 1; e < 16; ++e) t[e * ROW * 4 + lane] = r[e];
+    // The rows were written by other lanes of this wave, and the next group
+    // overwrites them after these reads: LDS executes a wave's operations in
+    // issue order, so only compiler motion is fenced (here and at the top).
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t word = SelWord(s, k >> 3);
+    const int e = (word >> (4 * (k & 7))) & 15;
+    const uint4* row = reinterpret_cast<const uint4*>(t) + e * ROW + cpart * CPL;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const uint4 v = row[c];
+      acc[4 * c] ^= v.x;
+      acc[4 * c + 1] ^= v.y;
+      acc[4 * c + 2] ^= v.z;
+      acc[4 * c + 3] ^= v.w;
+    }
+  }
+}
+
+#ifndef DPF_SCAN_M4_P1_WAVES
+#define DPF_SCAN_M4_P1_WAVES 3  // 168 VGPRs, 2 spilled
+#endif
+template <int P>
+__global__ __launch_bounds__(kScanM4Block, P == 1 ? DPF_SCAN_M4_P1_WAVES : P == 2 ? 4 : 6)
+void KPirScanM4(ScanArgs a) {
+  constexpr int QW = 64 / P;        // queries per wave
+  constexpr int CPL = 16 / P;       // 16-byte columns of the slice per lane
+  constexpr int ROW = 17;           // uint4 per table row (272 B)
+  __shared__ uint4 tab[kScanM4Waves][16 * ROW];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t part = (int64_t)blockIdx.x * kScanM4Waves + wave;
+  if (part >= a.parts) return;  // wave-uniform; no block barrier below
+  const int q = lane % QW, cpart = lane / QW;
+  const int dw_lo = blockIdx.y * 64;
+  const int width = min(64, a.C * 4 - dw_lo);  // dwords of this slice
+  const bool col_ok = lane < width;
+  const bool q_ok = q < a.nq;
+  uint32_t* t = reinterpret_cast<uint32_t*>(tab[wave]);
+  t[lane] = 0u;  // row 0 (no record selected) stays zero
+  uint32_t acc[4 * CPL];
+#pragma unroll
+  for (int i = 0; i < 4 * CPL; ++i) acc[i] = 0u;
+  const int64_t tiles = (a.num_records + 127) >> 7;
+  for (int64_t tile = part; tile < tiles; tile += a.parts) {
+    const uint4 s = q_ok ? a.sel[(int64_t)(a.q0 + q) * a.sel_blocks + tile]
+                         : make_uint4(0, 0, 0, 0);
+    if ((tile << 7) + 128 <= a.num_records)
+      ScanM4Tile<P, true>(a, tile, s, acc, t, lane, cpart, col_ok, dw_lo);
+    else
+      ScanM4Tile<P, false>(a, tile, s, acc, t, lane, cpart, col_ok, dw_lo);
+  }
+  if (!q_ok) return;
+  // this lane's columns [cpart * CPL, +CPL) of the slice, clipped to the record
+  uint4* out = a.partials + (part * a.total_q + a.q0 + q) * a.C + blockIdx.y * 16;
+  const int chunks = (width + 3) / 4;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = cpart * CPL + c;
+    if (col < chunks)
+      out[col] = make_uint4(acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]);
+  }
+}
+
+int LaunchPirScanM4(int P, int parts, int slices, hipStream_t st, const ScanArgs& a) {
+  const dim3 g((parts + kScanM4Waves - 1) / kScanM4Waves, slices);
+  if (P == 1)
+    hipLaunchKernelGGL((KPirScanM4<1>), g, dim3(kScanM4Block), 0, st, a);
+  else if (P == 2)
+    hipLaunchKernelGGL((KPirScanM4<2>), g, dim3(kScanM4Block), 0, st, a);
+  else
+    hipLaunchKernelGGL((KPirScanM4<4>), g, dim3(kScanM4Block), 0, st, a);
+  return LaunchCheck("pir scan kernel launch");
+}
+
 int LaunchGatherRows(int grid, hipStream_t st, int64_t n, const int64_t* src_offset,
                      int64_t opp, int64_t stride, const char* in, char* out, int64_t in_rows,
                      int* err) {

@@ -116,7 +116,18 @@ struct ScanArgs {
   int32_t q0;           // first query of this pass
   int32_t nq;           // queries in this pass (<= QN)
   int32_t total_q;
+  int32_t parts;        // partials written per query (KPirScanM4: waves in use)
 };
+
+// KPirScanM4: 4 independent waves per block, one LDS table pair per wave.
+constexpr int kScanM4Block = 256;
+constexpr int kScanM4Waves = kScanM4Block / 64;
+// Queries from which a scan pass uses KPirScanM4 (records of >= 64 bytes).
+// c4 (2^26 x 256 B): Q = 8 masked 2.55 ms vs M4 3.15; Q = 16 3.31 vs 2.91.
+#ifndef DPF_AMD_SCAN_M4_MIN_Q
+#define DPF_AMD_SCAN_M4_MIN_Q 16
+#endif
+constexpr int kScanM4MinQueries = DPF_AMD_SCAN_M4_MIN_Q;
 
 inline int HipCheck(hipError_t e, const char* what) {
   if (e == hipSuccess) return DPF_AMD_OK;
@@ -159,5 +170,8 @@ int LaunchPirScan(int nq, dim3 grid, hipStream_t st, const ScanArgs& a);
 // queries per scan pass = PirScanQueries(C).
 int PirScanGroup(int C);
 inline int PirScanQueries(int) { return 16; }
+// Four-Russians scan of 64 / P queries per pass (P in {1, 2, 4}) over
+// `slices` 256-byte column slices of the record.
+int LaunchPirScanM4(int P, int parts, int slices, hipStream_t st, const ScanArgs& a);
 
 }  // namespace dpf_amd

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -19,6 +20,10 @@ namespace dpf_amd {
 namespace {
 
 std::atomic<int> g_expand_depth{0};  // dpf_amd_set_expand_depth (tests)
+std::atomic<int> g_scan_m4{[] {      // dpf_amd_set_scan_m4 (tests, A/B)
+  const char* e = std::getenv("DPF_AMD_SCAN_M4");
+  return e ? std::atoi(e) : -1;
+}()};
 
 int GridFor(int64_t items, int block, int max_blocks) {
   int64_t g = (items + block - 1) / block;
@@ -262,6 +267,11 @@ int dpf_amd_set_expand_depth(int depth) {
   return g_expand_depth.exchange(depth);
 }
 
+int dpf_amd_set_scan_m4(int mode) {
+  if (mode < -1 || mode > 1) return -2;
+  return g_scan_m4.exchange(mode);
+}
+
 // Shared body of dpf_amd_evaluate_points{,_batched}.
 static int EvaluatePoints(int64_t num_points, int64_t points_per_key, int64_t num_cw,
                           const void* seeds, const uint8_t* control_bits, const void* paths,
@@ -407,15 +417,28 @@ int dpf_amd_xor_fold(const void* parts, int num_parts, int64_t bytes, void* out,
 }
 
 static int ScanGrid(int64_t num_records, int num_queries, int64_t record_stride) {
-  // At least one 128-record tile per wave; up to 8192 blocks (c4 Q = 8:
-  // 2.95 ms vs 3.17 ms at 2048 — more, shorter blocks balance across CUs),
-  // but at most 64 MiB of partials (grid x queries x record bytes) for the
-  // fold, and never fewer than 2048 blocks.
+  // At least one 128-record tile per wave; up to 8192 blocks / partials
+  // (c4 Q = 8: 2.95 ms vs 3.17 ms at 2048 — more, shorter blocks balance
+  // across CUs; KPirScanM4 at Q = 100: 2621 waves for 2048 resident slots
+  // left a 28 % second round), but at most 256 MiB of partials (grid x
+  // queries x record bytes) for the fold, and never fewer than 2048.
   const int64_t tiles = (num_records + 127) / 128;
   const int64_t g = (tiles + kScanWaves - 1) / kScanWaves;
   const int64_t per_block = std::max<int64_t>(1, (int64_t)num_queries * record_stride);
-  const int64_t cap = std::max<int64_t>(2048, std::min<int64_t>(8192, (64ll << 20) / per_block));
+  const int64_t cap = std::max<int64_t>(2048, std::min<int64_t>(8192, (256ll << 20) / per_block));
   return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+// Column parts P of the Four-Russians scan (KPirScanM4: 64 / P queries per
+// pass) for `rem` queries still to scan over C-chunk records, or 0 for the
+// masked scan (KPirScanG).  Mode (dpf_amd_set_scan_m4 / DPF_AMD_SCAN_M4):
+// 0 never, 1 always (tests), -1 from kScanM4MinQueries queries on.
+static int ScanM4Parts(int rem, int C) {
+  const int mode = g_scan_m4.load();
+  if (mode == 0) return 0;
+  if (C > (1 << 16)) return 0;  // records > 1 MiB: 128-record tiles past 2^27 B
+  if (mode < 0 && (rem < kScanM4MinQueries || C < 4)) return 0;
+  return rem > 32 ? 1 : rem > 16 ? 2 : 4;
 }
 
 int64_t dpf_amd_inner_product_workspace_size(int64_t num_records, int64_t record_stride,
@@ -449,13 +472,17 @@ int dpf_amd_inner_product(const void* db, int64_t num_records, int64_t record_st
   a.sel_blocks = selection_blocks;
   a.C = C;
   a.total_q = num_queries;
+  a.parts = grid;
   const dim3 g(grid, (C + 63) / 64);
-  for (int q0 = 0; q0 < num_queries; q0 += per_pass) {
-    const int nq = std::min(per_pass, num_queries - q0);
+  for (int q0 = 0; q0 < num_queries;) {
+    const int rem = num_queries - q0;
+    const int P = ScanM4Parts(rem, C);
+    const int nq = std::min(P ? 64 / P : per_pass, rem);
     a.q0 = q0;
     a.nq = nq;
-    int rc = LaunchPirScan(nq, g, st, a);
+    int rc = P ? LaunchPirScanM4(P, grid, (C + 15) / 16, st, a) : LaunchPirScan(nq, g, st, a);
     if (rc != DPF_AMD_OK) return rc;
+    q0 += nq;
   }
   return dpf_amd_xor_fold(workspace, grid, (int64_t)num_queries * record_stride, out, stream);
 }

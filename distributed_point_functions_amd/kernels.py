@@ -116,6 +116,24 @@ class forced_expand_depth:
         _lib.lib().dpf_amd_set_expand_depth(self.prev)
 
 
+class forced_scan_m4:
+    """Context manager selecting dpf_amd_inner_product's scan kernel
+    (dpf_amd_set_scan_m4: -1 automatic, 0 masked scan, 1 Four-Russians)."""
+
+    def __init__(self, mode: int):
+        self.mode = mode
+
+    def __enter__(self):
+        prev = _lib.lib().dpf_amd_set_scan_m4(self.mode)
+        if prev < -1:
+            raise ValueError("scan mode must be -1, 0 or 1")
+        self.prev = prev
+        return self
+
+    def __exit__(self, *exc):
+        _lib.lib().dpf_amd_set_scan_m4(self.prev)
+
+
 def evaluate_points(seeds, control_bits, paths, paths_rightshift, num_levels,
                     cw_seeds, ccl, ccr, desc, block_index=None, party=None,
                     party_all: int = 0, value_corrections=None,

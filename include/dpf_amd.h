@@ -138,6 +138,13 @@ int dpf_amd_expand_and_correct(
  * an invalid depth (setting unchanged). */
 int dpf_amd_set_expand_depth(int depth);
 
+/* Testing knob (process-wide): which XOR scan dpf_amd_inner_product runs.
+ * -1 automatic (the Four-Russians many-query scan from 16 queries on, records
+ * of >= 64 bytes; the masked scan otherwise), 0 always the masked scan, 1
+ * always the Four-Russians scan.  The default comes from DPF_AMD_SCAN_M4.
+ * Returns the previous setting, or -2 for an invalid mode (unchanged). */
+int dpf_amd_set_scan_m4(int mode);
+
 /* Fused single-path evaluation: EvaluateSeeds from the given seeds along
  * `paths` (one AES per level, per-lane key select) + HashExpandedSeeds +
  * correction of element block_index[i] (EvaluateAtImpl h:1013-1063 and the

@@ -342,14 +342,16 @@ def test_gather_rows(K, cuda, stride, opp):
 # Dense PIR scan vs oracle InnerProduct
 # ---------------------------------------------------------------------------
 
-@pytest.mark.parametrize("n,size,q", [(1, 16, 1), (1000, 256, 1), (1000, 256, 3),
-                                      (4096, 80, 8), (300, 17, 2), (777, 1104, 5),
-                                      (129, 4096, 1), (5000, 64, 11),
-                                      # many-query (Four Russians) scan: > 16 queries,
-                                      # records a multiple of 256 B
-                                      (1000, 256, 17), (3001, 256, 32), (4097, 512, 33),
-                                      (130, 256, 64), (2500, 768, 100)])
-def test_inner_product_matches_oracle(K, cuda, n, size, q):
+SCAN_CASES = [(1, 16, 1), (1000, 256, 1), (1000, 256, 3), (4096, 80, 8), (300, 17, 2),
+              (777, 1104, 5), (129, 4096, 1), (5000, 64, 11),
+              # many-query passes: Four-Russians P = 4 / 2 / 1 (16 / 32 / 64
+              # queries per pass), ragged tiles, several 256-B slices, a
+              # narrow last slice (1104 B = 4 x 256 + 80), 100 queries
+              (1000, 256, 17), (3001, 256, 32), (4097, 512, 33), (130, 256, 64),
+              (2500, 768, 100), (2049, 1104, 40), (640, 240, 16), (385, 64, 9)]
+
+
+def _scan_case(K, cuda, n, size, q, mode):
     import torch
     rng = np.random.default_rng(n * 7 + size)
     stride = (size + 15) // 16 * 16
@@ -357,12 +359,28 @@ def test_inner_product_matches_oracle(K, cuda, n, size, q):
     db = np.zeros((n, stride), dtype=np.uint8)
     db[:, :size] = recs
     blocks = (n + 127) // 128 + 1
-    sel_words = rng.integers(0, 2**63, size=(q * blocks, 2), dtype=np.int64)
-    sels = [[int(sel_words[k * blocks + i, 0]) | (int(sel_words[k * blocks + i, 1]) << 64)
+    # full-range words: every selection bit position (incl. 63 / 127) is exercised
+    sel_words = rng.integers(0, 2**64, size=(q * blocks, 2), dtype=np.uint64).view(np.int64)
+    sels = [[(int(sel_words[k * blocks + i, 0]) & M64) | ((int(sel_words[k * blocks + i, 1]) & M64) << 64)
              for i in range(blocks)] for k in range(q)]
     want = po.inner_product([bytes(r) for r in recs], sels)
-    out = K.inner_product(torch.from_numpy(db).to(cuda), n, stride,
-                          torch.from_numpy(sel_words).to(cuda), q)
+    with K.forced_scan_m4(mode):
+        out = K.inner_product(torch.from_numpy(db).to(cuda), n, stride,
+                              torch.from_numpy(sel_words).to(cuda), q)
     got = out.cpu().numpy().reshape(q, stride)[:, :size]
     for k in range(q):
         assert bytes(got[k]) == want[k], k
+
+
+@pytest.mark.parametrize("n,size,q", SCAN_CASES)
+def test_inner_product_matches_oracle(K, cuda, n, size, q):
+    """Automatic kernel choice (the production path)."""
+    _scan_case(K, cuda, n, size, q, -1)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("n,size,q", SCAN_CASES)
+def test_inner_product_each_scan_kernel(K, cuda, n, size, q, mode):
+    """Masked scan (KPirScanG) and Four-Russians scan (KPirScanM4) forced on
+    every shape, including the ones the automatic choice never gives them."""
+    _scan_case(K, cuda, n, size, q, mode)

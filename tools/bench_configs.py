@@ -277,6 +277,14 @@ def c4q(dev, reps):
         res["q%d_db_GBps" % q] = n * rec / t / 1e9
         res["q%d_hbm_frac" % q] = (n * rec + q * n // 8) / t / 8e12
         res["q%d_query_GBps" % q] = q * n * rec / t / 1e9
+        if q >= 8:
+            # A/B of the two scan kernels (automatic choice timed above)
+            ref = out.clone()
+            for mode, name in ((0, "masked"), (1, "m4")):
+                with kernels.forced_scan_m4(mode):
+                    tm = ev_time(scan, reps)
+                    res["q%d_%s_ms" % (q, name)] = tm * 1e3
+                    res["q%d_%s_equal" % (q, name)] = bool(torch.equal(out, ref))
     del db
     return res
 
