@@ -327,6 +327,24 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
 // LDS traffic per 4 records: 15 row stores (64 lanes x 4 B) + QW rows read
 // (256 B each); VALU: 11 + 2 + 64 XORs per lane.  Records past num_records
 // and slice dwords past the record read as zero, so they add nothing.
+//
+// Measured on MI355X, c4 (2^26 x 256 B), Q = 64 (masked scan: 15.0 ms):
+// this kernel 4.50 ms with ds_write_addtid row stores, 4.79 ms with
+// ds_write2_b32 stores (7 address VGPRs).  Rejected: deeper register
+// prefetch (2 / 4 groups at 2 waves/SIMD: 5.29 / 5.54 ms), row reads in
+// batches of 4 (4.90), and tables shared by a block's waves (16 queries per
+// wave, one LDS barrier per group, 8 waves/SIMD: 6.97 ms; Q = 100 in one
+// pass 15.6 ms vs 9.2 in two per-wave passes).
+#ifndef DPF_SCAN_M4_ADDTID
+#define DPF_SCAN_M4_ADDTID 1  // row stores as ds_write_addtid_b32 (inline asm)
+#endif
+#ifndef DPF_SCAN_M4_PREFETCH
+#define DPF_SCAN_M4_PREFETCH 1  // 4-record groups in flight per wave
+#endif
+#ifndef DPF_SCAN_M4_READ_BATCH
+#define DPF_SCAN_M4_READ_BATCH 16  // ds_read_b128 issued back to back
+#endif
+
 // One 128-record tile.  FULL tiles read the records through a buffer
 // resource based at the tile (record offsets in SGPRs, nontemporal); the
 // last, partial tile reads records past num_records as zero.
@@ -339,21 +357,30 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
   const int rec_dwords = a.C * 4;
   const int64_t rec0 = tile << 7;
   const uint32_t* base = reinterpret_cast<const uint32_t*>(a.db) + rec0 * rec_dwords + dw_lo;
-  const __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
-  // lanes past the slice's width read beyond num_records (0x7fffffff): zero.
-  // Record offsets go in soffset (< 128 * rec_bytes <= 2^27, see ScanM4Parts).
+  // The last, partial tile limits the range to the bytes left after `base`
+  // and puts the record offset in voffset, which the range check covers:
+  // records past num_records read as zero.
+  const int64_t left = (a.num_records - rec0) * rec_dwords * 4 - dw_lo * 4;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)base, 0, FULL ? 0x7fffffff : (int)left, 0x00020000);
+  // lanes past the slice's width read beyond num_records (<= 0x7fffffff): zero.
+  // Record offsets stay below 128 * rec_bytes <= 2^27 (see ScanM4Parts).
   const int voff = col_ok ? lane * 4 : (int)0x80000000u;
   auto load = [&](int r) -> uint32_t {
     if constexpr (FULL) {
       return __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, r * rec_dwords * 4, 2);
     } else {
-      return (col_ok && rec0 + r < a.num_records) ? base[(int64_t)r * rec_dwords + lane] : 0u;
+      return __builtin_amdgcn_raw_buffer_load_b32(
+          rsrc, col_ok ? r * rec_dwords * 4 + lane * 4 : (int)0x80000000u, 0, 2);
     }
   };
-  uint32_t xn[4];
+  // records of the next PF groups in flight (a rotating register queue);
+  // the last groups re-read the tile's first, cached, records rather than
+  // branching
+  constexpr int PF = DPF_SCAN_M4_PREFETCH;
+  uint32_t xq[4 * PF];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) xn[i] = load(i);
+  for (int i = 0; i < 4 * PF; ++i) xq[i] = load(i);
 #pragma unroll 1
   for (int k = 0; k < 32; ++k) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -361,18 +388,40 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     uint32_t x[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) x[i] = xn[i];
-    // next group (the last group re-reads the tile's first, cached, records
-    // rather than branching)
+    for (int i = 0; i < 4; ++i) x[i] = xq[i];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xn[i] = load((4 * (k + 1) + i) & 127);
+    for (int i = 0; i < 4 * (PF - 1); ++i) xq[i] = xq[i + 4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xq[4 * (PF - 1) + i] = load((4 * (k + PF) + i) & 127);
     const uint32_t x01 = x[0] ^ x[1], x012 = x01 ^ x[2];
     const uint32_t r[16] = {0u,          x[0],        x[1],        x01,
                             x[2],        x[0] ^ x[2], x[1] ^ x[2], x012,
                             x[3],        x[0] ^ x[3], x[1] ^ x[3], x01 ^ x[3],
                             x[2] ^ x[3], x[0] ^ x[2] ^ x[3], x[1] ^ x[2] ^ x[3], x012 ^ x[3]};
+#if DPF_SCAN_M4_ADDTID
+    // ds_write_addtid_b32 (address = M0 + offset + 4 * lane): no address
+    // VGPRs and half the LDS transfer cycles of ds_write_b32.  M0 is set in
+    // the same asm statement, so no compiler-held M0 value is assumed after.
+    asm volatile(
+        "s_mov_b32 m0, %15\n\t"
+        "ds_write_addtid_b32 %0 offset:272\n\tds_write_addtid_b32 %1 offset:544\n\t"
+        "ds_write_addtid_b32 %2 offset:816\n\tds_write_addtid_b32 %3 offset:1088\n\t"
+        "ds_write_addtid_b32 %4 offset:1360\n\tds_write_addtid_b32 %5 offset:1632\n\t"
+        "ds_write_addtid_b32 %6 offset:1904\n\tds_write_addtid_b32 %7 offset:2176\n\t"
+        "ds_write_addtid_b32 %8 offset:2448\n\tds_write_addtid_b32 %9 offset:2720\n\t"
+        "ds_write_addtid_b32 %10 offset:2992\n\tds_write_addtid_b32 %11 offset:3264\n\t"
+        "ds_write_addtid_b32 %12 offset:3536\n\tds_write_addtid_b32 %13 offset:3808\n\t"
+        "ds_write_addtid_b32 %14 offset:4080"
+        :
+        : "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]),
+          "v"(r[8]), "v"(r[9]), "v"(r[10]), "v"(r[11]), "v"(r[12]), "v"(r[13]), "v"(r[14]),
+          "v"(r[15]), "s"((uint32_t)(uintptr_t)t)
+        : "memory");
+    static_assert(ROW * 16 == 272, "addtid offsets assume 272-byte rows");
+#else
 #pragma unroll
     for (int e = 1; e < 16; ++e) t[e * ROW * 4 + lane] = r[e];
+#endif
     // The rows were written by other lanes of this wave, and the next group
     // overwrites them after these reads: LDS executes a wave's operations in
     // issue order, so only compiler motion is fenced (here and at the top).
@@ -382,19 +431,26 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
     const uint32_t word = SelWord(s, k >> 3);
     const int e = (word >> (4 * (k & 7))) & 15;
     const uint4* row = reinterpret_cast<const uint4*>(t) + e * ROW + cpart * CPL;
+    // row reads in batches of RB (their destination VGPRs are what bounds
+    // the wave's register budget)
+    constexpr int RB = CPL < DPF_SCAN_M4_READ_BATCH ? CPL : DPF_SCAN_M4_READ_BATCH;
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      const uint4 v = row[c];
-      acc[4 * c] ^= v.x;
-      acc[4 * c + 1] ^= v.y;
-      acc[4 * c + 2] ^= v.z;
-      acc[4 * c + 3] ^= v.w;
+    for (int c0 = 0; c0 < CPL; c0 += RB) {
+#pragma unroll
+      for (int c = c0; c < c0 + RB; ++c) {
+        const uint4 v = row[c];
+        acc[4 * c] ^= v.x;
+        acc[4 * c + 1] ^= v.y;
+        acc[4 * c + 2] ^= v.z;
+        acc[4 * c + 3] ^= v.w;
+      }
+      if (RB < CPL) __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
 
 #ifndef DPF_SCAN_M4_P1_WAVES
-#define DPF_SCAN_M4_P1_WAVES 3  // 168 VGPRs, 2 spilled
+#define DPF_SCAN_M4_P1_WAVES 3  // 163 VGPRs with the addtid stores
 #endif
 template <int P>
 __global__ __launch_bounds__(kScanM4Block, P == 1 ? DPF_SCAN_M4_P1_WAVES : P == 2 ? 4 : 6)
@@ -438,7 +494,10 @@ void KPirScanM4(ScanArgs a) {
   }
 }
 
-int LaunchPirScanM4(int P, int parts, int slices, hipStream_t st, const ScanArgs& a) {
+int PirScanM4Queries(int rem) { return std::min(rem, rem > 32 ? 64 : rem > 16 ? 32 : 16); }
+
+int LaunchPirScanM4(int nq, int parts, int slices, hipStream_t st, const ScanArgs& a) {
+  const int P = nq > 32 ? 1 : nq > 16 ? 2 : 4;
   const dim3 g((parts + kScanM4Waves - 1) / kScanM4Waves, slices);
   if (P == 1)
     hipLaunchKernelGGL((KPirScanM4<1>), g, dim3(kScanM4Block), 0, st, a);

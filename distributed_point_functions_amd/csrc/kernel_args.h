@@ -170,8 +170,10 @@ int LaunchPirScan(int nq, dim3 grid, hipStream_t st, const ScanArgs& a);
 // queries per scan pass = PirScanQueries(C).
 int PirScanGroup(int C);
 inline int PirScanQueries(int) { return 16; }
-// Four-Russians scan of 64 / P queries per pass (P in {1, 2, 4}) over
-// `slices` 256-byte column slices of the record.
-int LaunchPirScanM4(int P, int parts, int slices, hipStream_t st, const ScanArgs& a);
+// Four-Russians scan: queries of the next pass (of `rem` left), and the
+// launch of one pass of nq <= PirScanM4Queries(nq) queries over `slices`
+// 256-byte column slices of the record, writing `parts` partials per query.
+int PirScanM4Queries(int rem);
+int LaunchPirScanM4(int nq, int parts, int slices, hipStream_t st, const ScanArgs& a);
 
 }  // namespace dpf_amd

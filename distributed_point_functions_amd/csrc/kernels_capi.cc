@@ -429,16 +429,16 @@ static int ScanGrid(int64_t num_records, int num_queries, int64_t record_stride)
   return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
 }
 
-// Column parts P of the Four-Russians scan (KPirScanM4: 64 / P queries per
-// pass) for `rem` queries still to scan over C-chunk records, or 0 for the
-// masked scan (KPirScanG).  Mode (dpf_amd_set_scan_m4 / DPF_AMD_SCAN_M4):
-// 0 never, 1 always (tests), -1 from kScanM4MinQueries queries on.
-static int ScanM4Parts(int rem, int C) {
+// Whether the next pass over `rem` queries of C-chunk records runs the
+// Four-Russians scan (KPirScanM4*) rather than the masked scan (KPirScanG).
+// Mode (dpf_amd_set_scan_m4 / DPF_AMD_SCAN_M4): 0 never, 1 always (tests),
+// -1 from kScanM4MinQueries queries on.
+static bool UseScanM4(int rem, int C) {
   const int mode = g_scan_m4.load();
-  if (mode == 0) return 0;
-  if (C > (1 << 16)) return 0;  // records > 1 MiB: 128-record tiles past 2^27 B
-  if (mode < 0 && (rem < kScanM4MinQueries || C < 4)) return 0;
-  return rem > 32 ? 1 : rem > 16 ? 2 : 4;
+  if (mode == 0) return false;
+  if (C > (1 << 16)) return false;  // records > 1 MiB: 128-record tiles past 2^27 B
+  if (mode < 0 && (rem < kScanM4MinQueries || C < 4)) return false;
+  return true;
 }
 
 int64_t dpf_amd_inner_product_workspace_size(int64_t num_records, int64_t record_stride,
@@ -476,11 +476,11 @@ int dpf_amd_inner_product(const void* db, int64_t num_records, int64_t record_st
   const dim3 g(grid, (C + 63) / 64);
   for (int q0 = 0; q0 < num_queries;) {
     const int rem = num_queries - q0;
-    const int P = ScanM4Parts(rem, C);
-    const int nq = std::min(P ? 64 / P : per_pass, rem);
+    const bool m4 = UseScanM4(rem, C);
+    const int nq = m4 ? PirScanM4Queries(rem) : std::min(per_pass, rem);
     a.q0 = q0;
     a.nq = nq;
-    int rc = P ? LaunchPirScanM4(P, grid, (C + 15) / 16, st, a) : LaunchPirScan(nq, g, st, a);
+    int rc = m4 ? LaunchPirScanM4(nq, grid, (C + 15) / 16, st, a) : LaunchPirScan(nq, g, st, a);
     if (rc != DPF_AMD_OK) return rc;
     q0 += nq;
   }

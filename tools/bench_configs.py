@@ -257,13 +257,17 @@ def c3(dev, reps):
             "device_out_leaves_per_s": leaves / sum(best["device"]), "correct": bool(ok)}
 
 
+C4Q_QUERIES = (1, 8, 16, 32, 64, 100)
+C4Q_AB = True
+
+
 def c4q(dev, reps):
     n, rec = 1 << 26, 256
     gen = torch.Generator(device=dev)
     gen.manual_seed(4)
     db = torch.randint(0, 256, (n * rec,), dtype=torch.uint8, device=dev, generator=gen)
     res = {"config": "c4q", "workload": "XOR scan 2^26 x 256 B"}
-    for q in (1, 8, 16, 32, 64, 100):
+    for q in C4Q_QUERIES:
         sel = torch.randint(-2**63, 2**63 - 1, (q * (n // 128), 2), dtype=torch.int64,
                             device=dev, generator=gen)
         ws = torch.empty(max(16, _lib.lib().dpf_amd_inner_product_workspace_size(n, rec, q)),
@@ -277,7 +281,7 @@ def c4q(dev, reps):
         res["q%d_db_GBps" % q] = n * rec / t / 1e9
         res["q%d_hbm_frac" % q] = (n * rec + q * n // 8) / t / 8e12
         res["q%d_query_GBps" % q] = q * n * rec / t / 1e9
-        if q >= 8:
+        if q >= 8 and C4Q_AB:
             # A/B of the two scan kernels (automatic choice timed above)
             ref = out.clone()
             for mode, name in ((0, "masked"), (1, "m4")):
@@ -441,7 +445,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="c1,c2,c3,c4q,dcf,cuckoo")
     ap.add_argument("--reps", type=int, default=8)
+    ap.add_argument("--c4q-queries", default=None, help="comma list, e.g. 64 (profiling)")
+    ap.add_argument("--no-ab", action="store_true", help="c4q: skip the kernel A/B")
     args = ap.parse_args()
+    global C4Q_QUERIES, C4Q_AB
+    if args.c4q_queries:
+        C4Q_QUERIES = tuple(int(x) for x in args.c4q_queries.split(","))
+    C4Q_AB = not args.no_ab
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     for name in args.only.split(","):
