@@ -47,9 +47,11 @@ OPS_PER_AES = 757.5            # bitsliced AES-128 gate count
 LDS_LOOKUPS_PER_AES = 160      # T-table lookups per AES block
 LDS_PEAK_LOOKUPS = 256 * 32 * 2.4e9  # ds_read_b32: 32 lane-lookups/clk/CU
 AES_PER_LEAF_C5 = 4.0          # 2(2^32-1) tree + 2 * 2^32 value AES per 2^32 leaves
-# T-table lookups per c5 leaf: 2 x 160 (tree children) + 160 + 133 (the value
-# PRG pair seed, seed + 1 shares 27 lookups of rounds 1-2)
-LDS_LOOKUPS_PER_LEAF_C5 = 613
+# T-table lookups per c5 leaf: 2 x 160 (tree children) + 160 + 121 (the value
+# PRG pair seed, seed + 1 shares 27 lookups of rounds 1-2, and only word 0 of
+# the second value block is used: its last round is 4 lookups, not 16 —
+# DESIGN.md §3.1)
+LDS_LOOKUPS_PER_LEAF_C5 = 601
 
 
 def log(*a):
@@ -188,8 +190,27 @@ def bench_pir(args, world, rank, device):
     barrier(world)
     wall = max_over_ranks(time.perf_counter() - t0, world) / args.steps
     scan_ms = max_over_ranks(scan_ms / args.steps, world)
+    # a 64-query batch over the same resident rows (the reference batches up
+    # to 100 queries: pir/dense_dpf_pir_database_benchmark.cc): the
+    # Four-Russians scan (KPirScanM4), random selection shares
+    mq = 64
+    msel = torch.randint(-2**63, 2**63 - 1, (mq * max(1, b_hi - b_lo), 2), dtype=torch.int64,
+                         device=device, generator=gen)
+    mws = torch.empty(max(16, _lib.lib().dpf_amd_inner_product_workspace_size(per, rec, mq)),
+                      dtype=torch.uint8, device=device)
+    mout = torch.empty(mq * rec, dtype=torch.uint8, device=device)
+    kernels.inner_product(db, per, rec, msel, mq, mws, mout)
+    barrier(world)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(args.steps):
+        kernels.inner_product(db, per, rec, msel, mq, mws, mout)
+    ev[1].record()
+    barrier(world)
+    mq_ms = max_over_ranks(ev[0].elapsed_time(ev[1]) / args.steps, world)
+    del mws, msel
     return dict(ok=ok, wall_s=wall, scan_ms=scan_ms, db_bytes=n * rec, per_gpu_bytes=per * rec,
-                records=n)
+                records=n, mq=mq, mq_ms=mq_ms)
 
 
 def library_sha256():
@@ -308,7 +329,7 @@ def main():
                                       (args.log_domain, world)},
             # The T-table AES is bound by LDS lookup issue (ds_read_b32: 32
             # lane-lookups/clk/CU, conflict-free by construction): achieved =
-            # leaves per launch x 613 lookups / kernel time (the subtree walk's
+            # leaves per launch x 601 lookups / kernel time (the subtree walk's
             # extra lookups, ~0.3%, are not counted).
             "roofline": {"bound": "lds",
                          "achieved": lookups_s / 1e12,
@@ -345,6 +366,11 @@ def main():
                              "traffic": scan_traffic[0], "traffic_profile": scan_traffic[1],
                              "algorithmic_bytes": pir["per_gpu_bytes"],
                              "kernel": "KPirScanG<1,4>+KXorFold", "kernel_ms": pir["scan_ms"]},
+                "batch_%d" % pir["mq"]: {
+                    "queries": pir["mq"], "ms_per_batch": pir["mq_ms"],
+                    "query_GBps": pir["mq"] * pir["db_bytes"] / (pir["mq_ms"] / 1e3) / 1e9,
+                    "db_GBps": pir["db_bytes"] / (pir["mq_ms"] / 1e3) / 1e9,
+                    "kernel": "KPirScanM4<1>+KXorFold (scan only, no selection DPF)"},
             }
         print(json.dumps(out), flush=True)
     if world > 1:

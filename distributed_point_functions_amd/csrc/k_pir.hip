@@ -338,6 +338,12 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
 #ifndef DPF_SCAN_M4_ADDTID
 #define DPF_SCAN_M4_ADDTID 1  // row stores as ds_write_addtid_b32 (inline asm)
 #endif
+#ifndef DPF_SCAN_M4_WAIT_STORES
+#define DPF_SCAN_M4_WAIT_STORES 0  // drain the addtid stores inside their asm block
+#endif
+#ifndef DPF_SCAN_M4_DBUF
+#define DPF_SCAN_M4_DBUF 0  // diagnostics: alternate two tables per wave
+#endif
 #ifndef DPF_SCAN_M4_PREFETCH
 #define DPF_SCAN_M4_PREFETCH 1  // 4-record groups in flight per wave
 #endif
@@ -350,7 +356,7 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
 // last, partial tile reads records past num_records as zero.
 template <int P, bool FULL>
 __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint4 s,
-                                           uint32_t (&acc)[64 / P], uint32_t* t, int lane,
+                                           uint32_t (&acc)[64 / P], uint32_t* t_base, int lane,
                                            int cpart, bool col_ok, int dw_lo) {
   constexpr int CPL = 16 / P;
   constexpr int ROW = 17;
@@ -393,6 +399,7 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
     for (int i = 0; i < 4 * (PF - 1); ++i) xq[i] = xq[i + 4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) xq[4 * (PF - 1) + i] = load((4 * (k + PF) + i) & 127);
+    uint32_t* t = (DPF_SCAN_M4_DBUF && (k & 1)) ? t_base + 16 * ROW * 4 : t_base;
     const uint32_t x01 = x[0] ^ x[1], x012 = x01 ^ x[2];
     const uint32_t r[16] = {0u,          x[0],        x[1],        x01,
                             x[2],        x[0] ^ x[2], x[1] ^ x[2], x012,
@@ -401,9 +408,14 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
 #if DPF_SCAN_M4_ADDTID
     // ds_write_addtid_b32 (address = M0 + offset + 4 * lane): no address
     // VGPRs and half the LDS transfer cycles of ds_write_b32.  M0 is set in
-    // the same asm statement, so no compiler-held M0 value is assumed after.
+    // the same asm statement, so no compiler-held M0 value is assumed after;
+    // the compiler's hazard recognizer does not see inside the asm, so the
+    // wait state an add-TID op needs after an SALU write of M0 is explicit
+    // (without it, rows were written elsewhere at random: nondeterministic
+    // 2^26-record scans, tools/diag_scan_determinism.py).
     asm volatile(
         "s_mov_b32 m0, %15\n\t"
+        "s_nop 0\n\t"  // SALU write of M0 -> LDS add-TID op: 1 wait state
         "ds_write_addtid_b32 %0 offset:272\n\tds_write_addtid_b32 %1 offset:544\n\t"
         "ds_write_addtid_b32 %2 offset:816\n\tds_write_addtid_b32 %3 offset:1088\n\t"
         "ds_write_addtid_b32 %4 offset:1360\n\tds_write_addtid_b32 %5 offset:1632\n\t"
@@ -412,6 +424,9 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
         "ds_write_addtid_b32 %10 offset:2992\n\tds_write_addtid_b32 %11 offset:3264\n\t"
         "ds_write_addtid_b32 %12 offset:3536\n\tds_write_addtid_b32 %13 offset:3808\n\t"
         "ds_write_addtid_b32 %14 offset:4080"
+#if DPF_SCAN_M4_WAIT_STORES
+        "\n\ts_waitcnt lgkmcnt(0)"
+#endif
         :
         : "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]),
           "v"(r[8]), "v"(r[9]), "v"(r[10]), "v"(r[11]), "v"(r[12]), "v"(r[13]), "v"(r[14]),
@@ -458,7 +473,7 @@ void KPirScanM4(ScanArgs a) {
   constexpr int QW = 64 / P;        // queries per wave
   constexpr int CPL = 16 / P;       // 16-byte columns of the slice per lane
   constexpr int ROW = 17;           // uint4 per table row (272 B)
-  __shared__ uint4 tab[kScanM4Waves][16 * ROW];
+  __shared__ uint4 tab[kScanM4Waves][1 + DPF_SCAN_M4_DBUF][16 * ROW];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t part = (int64_t)blockIdx.x * kScanM4Waves + wave;
@@ -468,8 +483,9 @@ void KPirScanM4(ScanArgs a) {
   const int width = min(64, a.C * 4 - dw_lo);  // dwords of this slice
   const bool col_ok = lane < width;
   const bool q_ok = q < a.nq;
-  uint32_t* t = reinterpret_cast<uint32_t*>(tab[wave]);
+  uint32_t* t = reinterpret_cast<uint32_t*>(tab[wave][0]);
   t[lane] = 0u;  // row 0 (no record selected) stays zero
+  if (DPF_SCAN_M4_DBUF) reinterpret_cast<uint32_t*>(tab[wave][DPF_SCAN_M4_DBUF])[lane] = 0u;
   uint32_t acc[4 * CPL];
 #pragma unroll
   for (int i = 0; i < 4 * CPL; ++i) acc[i] = 0u;

@@ -384,3 +384,28 @@ def test_inner_product_each_scan_kernel(K, cuda, n, size, q, mode):
     """Masked scan (KPirScanG) and Four-Russians scan (KPirScanM4) forced on
     every shape, including the ones the automatic choice never gives them."""
     _scan_case(K, cuda, n, size, q, mode)
+
+
+@pytest.mark.parametrize("n,size,qs", [(1 << 22, 256, (16, 40, 64, 100)),
+                                       (1 << 18, 1104, (33,))])
+def test_scan_kernels_agree_large(K, cuda, n, size, qs):
+    """Random full selections over millions of records: the Four-Russians
+    scan equals the masked scan (each pinned to the oracle above) and repeats
+    bit-identically.  Small cases cannot show a table row written to the wrong
+    place at random (an add-TID store issued without its M0 wait state gave
+    exactly that at 2^26 records)."""
+    import torch
+    stride = (size + 15) // 16 * 16
+    gen = torch.Generator(device=cuda)
+    gen.manual_seed(n + size)
+    db = torch.randint(0, 256, (n * stride,), dtype=torch.uint8, device=cuda, generator=gen)
+    blocks = (n + 127) // 128
+    for q in qs:
+        sel = torch.randint(-2**63, 2**63 - 1, (q * blocks, 2), dtype=torch.int64, device=cuda,
+                            generator=gen)
+        outs = []
+        for mode in (0, 1, 1):
+            with K.forced_scan_m4(mode):
+                outs.append(K.inner_product(db, n, stride, sel, q).clone())
+        assert torch.equal(outs[1], outs[2]), "Four-Russians scan not repeatable (q=%d)" % q
+        assert torch.equal(outs[0], outs[1]), "Four-Russians scan != masked scan (q=%d)" % q

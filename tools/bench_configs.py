@@ -441,9 +441,24 @@ def cuckoo(dev, reps):
             "db_build_s": t_build, "served": served, "correct": bool(ok)}
 
 
+def cpp(dev, reps):
+    """c1-c3 through the C++ API (tools/cpp_api_bench.cc, built by
+    build_native against include/ and libdpf_amd.so) — what a reference
+    caller would see; one JSON line per config."""
+    import subprocess
+    from distributed_point_functions_amd import build_native
+    torch.cuda.synchronize()
+    res = subprocess.run([build_native.CPP_BENCH, str(reps)], capture_output=True, text=True,
+                         timeout=600)
+    if res.returncode != 0:
+        raise RuntimeError("cpp_api_bench failed: " + res.stderr[-2000:])
+    lines = [json.loads(x) for x in res.stdout.splitlines() if x.startswith("{")]
+    return {"config": "cpp", "workload": "C++ API c1-c3", "results": lines}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="c1,c2,c3,c4q,dcf,cuckoo")
+    ap.add_argument("--only", default="c1,c2,c3,c4q,dcf,cuckoo,cpp")
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--c4q-queries", default=None, help="comma list, e.g. 64 (profiling)")
     ap.add_argument("--no-ab", action="store_true", help="c4q: skip the kernel A/B")
