@@ -16,7 +16,7 @@ namespace distributed_point_functions {
 
 using dpf_internal_host::AbiStatus;
 using dpf_internal_host::ClearPadding;
-using dpf_internal_host::CopyToHost;
+using dpf_internal_host::CopyToHostSync;
 using dpf_internal_host::DeviceBuffer;
 using dpf_internal_host::HipStatus;
 using dpf_internal_host::ThreadStream;
@@ -170,8 +170,7 @@ Status DistributedComparisonFunction::BatchEvaluateRaw(Span<const DcfKey* const>
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_dcf_evaluate(
       n, dseeds.get(), dcbs.as<uint8_t>(), dparty.as<int8_t>(), dpoints.get(), H, tree_of.data(),
       dcws.get(), dccl.as<uint8_t>(), dccr.as<uint8_t>(), &vt, dcorr.get(), dout.get(), s)));
-  DPF_RETURN_IF_ERROR(CopyToHost(out, dout.get(), n * vt.out_stride, s));
-  return HipStatus(hipStreamSynchronize(s), "sync");
+  return CopyToHostSync(out, dout.get(), n * vt.out_stride, s);
 }
 
 }  // namespace distributed_point_functions

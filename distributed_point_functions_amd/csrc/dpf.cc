@@ -718,6 +718,7 @@ bool DistributedPointFunction::IsValueTypeRegistered(const ValueType& value_type
 using dpf_internal_host::AbiStatus;
 using dpf_internal_host::ClearPadding;
 using dpf_internal_host::CopyToHost;
+using dpf_internal_host::CopyToHostSync;
 using dpf_internal_host::DeviceBuffer;
 using dpf_internal_host::HipStatus;
 using dpf_internal_host::HostTrace;
@@ -1326,8 +1327,9 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
     DPF_RETURN_IF_ERROR(CopyToHost(&gather_flag, gather_err.get(), sizeof(int), s));
   }
   if (!out_on_device)
-    DPF_RETURN_IF_ERROR(CopyToHost(out, final_dev, total * stride, s));
-  DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+    DPF_RETURN_IF_ERROR(CopyToHostSync(out, final_dev, total * stride, s));
+  else
+    DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
   if (gather_flag) {  // the offsets were checked on the host: the device copy differs
     std::string detail;
     if (!prefixes.empty()) {
@@ -1414,8 +1416,7 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
       n, seeds.get(), cbs.as<uint8_t>(), paths.get(), 0, levels, levels, cws.get(),
       ccl.as<uint8_t>(), ccr.as<uint8_t>(), &vt, bi.as<uint8_t>(), nullptr, key.party(), nullptr,
       reinterpret_cast<const uint64_t*>(corr.data()), dout.get(), nullptr, nullptr, s)));
-  DPF_RETURN_IF_ERROR(CopyToHost(out, dout.get(), n * vt.out_stride, s));
-  DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+  DPF_RETURN_IF_ERROR(CopyToHostSync(out, dout.get(), n * vt.out_stride, s));
   if (ctx) ctx->set_previous_hierarchy_level(hierarchy_level);
   return OkStatus();
 }
@@ -1496,9 +1497,8 @@ Status DistributedPointFunction::EvaluateAndApplyRaw(Span<const DpfKey* const> k
         static_cast<int64_t>(levels) * n, dcws.get(), dccl.as<uint8_t>(), dccr.as<uint8_t>(),
         &vt, dbi.as<uint8_t>(), pty.as<int8_t>(), 0, dcorr.get(), nullptr, dout.get(),
         seeds.get(), cbs.as<uint8_t>(), s)));
-    DPF_RETURN_IF_ERROR(CopyToHost(host_out + h * n * vt.out_stride, dout.get(),
-                                                 n * vt.out_stride, s));
-    DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+    DPF_RETURN_IF_ERROR(
+        CopyToHostSync(host_out + h * n * vt.out_stride, dout.get(), n * vt.out_stride, s));
     *levels_done = h + 1;
     // h:1190-1196: stop as soon as `op` returns false (the remaining levels
     // are never evaluated)

@@ -5,7 +5,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <thread>
 #include <map>
 #include <mutex>
 #include <unordered_map>
@@ -80,6 +83,131 @@ inline Status CopyToHost(void* dst, const void* src, size_t bytes, hipStream_t s
   static const bool drain = std::getenv("DPF_AMD_SYNC_D2H") != nullptr;
   if (drain) DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
   return HipStatus(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s), "d2h");
+}
+
+// Host memcpy split over a few persistent worker threads: one thread copies
+// from pinned into pageable memory at ~8 GB/s, below the PCIe DMA rate.
+class MemcpyPool {
+ public:
+  static MemcpyPool& Get() {
+    static MemcpyPool* pool = new MemcpyPool();  // never destroyed: workers live to exit
+    return *pool;
+  }
+  void Copy(char* dst, const char* src, size_t bytes) {
+    const size_t parts = std::min<size_t>(kWorkers + 1, std::max<size_t>(1, bytes >> 20));
+    if (parts <= 1) {
+      std::memcpy(dst, src, bytes);
+      return;
+    }
+    std::lock_guard<std::mutex> one(call_mu_);  // one copy in flight at a time
+    const size_t per = (bytes + parts - 1) / parts;
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      dst_ = dst;
+      src_ = src;
+      bytes_ = bytes;
+      per_ = per;
+      next_ = 1;
+      parts_ = parts;
+      pending_ = parts - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    std::memcpy(dst, src, std::min(per, bytes));  // part 0 on the caller
+    std::unique_lock<std::mutex> l(mu_);
+    done_cv_.wait(l, [&] { return pending_ == 0; });
+  }
+
+ private:
+  static constexpr size_t kWorkers = 7;
+  MemcpyPool() {
+    for (size_t i = 0; i < kWorkers; ++i) std::thread([this] { Work(); }).detach();
+  }
+  void Work() {
+    uint64_t seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> l(mu_);
+      cv_.wait(l, [&] { return gen_ != seen && next_ < parts_; });
+      seen = gen_;
+      while (next_ < parts_) {
+        const size_t i = next_++;
+        const size_t off = i * per_;
+        char* d = dst_;
+        const char* sr = src_;
+        const size_t n = off < bytes_ ? std::min(per_, bytes_ - off) : 0;
+        l.unlock();
+        if (n) std::memcpy(d + off, sr + off, n);
+        l.lock();
+        if (--pending_ == 0) done_cv_.notify_one();
+      }
+    }
+  }
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  char* dst_ = nullptr;
+  const char* src_ = nullptr;
+  size_t bytes_ = 0, per_ = 0, next_ = 0, parts_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+};
+
+// Device-to-host copy into pageable `dst`, complete on return.  A plain
+// hipMemcpy into pageable memory stages through the runtime's own small
+// pinned buffers one after the other; large copies here go through two
+// pinned 16 MiB chunks per thread, the DMA of chunk i + 1 overlapping the
+// host memcpy of chunk i (c3: 128 MiB per level).
+class D2HStaging {
+ public:
+  static constexpr size_t kChunk = 16u << 20;
+  D2HStaging() = default;
+  D2HStaging(const D2HStaging&) = delete;
+  D2HStaging& operator=(const D2HStaging&) = delete;
+  ~D2HStaging() {
+    for (int i = 0; i < 2; ++i) {
+      if (ev_[i]) {
+        (void)hipEventSynchronize(ev_[i]);
+        (void)hipEventDestroy(ev_[i]);
+      }
+      if (pin_[i]) (void)hipHostFree(pin_[i]);
+    }
+  }
+  Status Copy(char* dst, const char* src, size_t bytes, hipStream_t s) {
+    for (int i = 0; i < 2; ++i) {
+      if (!pin_[i])
+        DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc(&pin_[i], kChunk, 0), "hipHostMalloc"));
+      if (!ev_[i])
+        DPF_RETURN_IF_ERROR(
+            HipStatus(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "hipEventCreate"));
+    }
+    const size_t n = (bytes + kChunk - 1) / kChunk;
+    auto len = [&](size_t i) { return std::min(kChunk, bytes - i * kChunk); };
+    for (size_t i = 0; i <= n; ++i) {
+      if (i < n) {
+        DPF_RETURN_IF_ERROR(HipStatus(hipMemcpyAsync(pin_[i & 1], src + i * kChunk, len(i),
+                                                     hipMemcpyDeviceToHost, s),
+                                      "d2h"));
+        DPF_RETURN_IF_ERROR(HipStatus(hipEventRecord(ev_[i & 1], s), "hipEventRecord"));
+      }
+      if (i >= 1) {
+        const size_t j = i - 1;
+        DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(ev_[j & 1]), "d2h"));
+        MemcpyPool::Get().Copy(dst + j * kChunk, static_cast<const char*>(pin_[j & 1]), len(j));
+      }
+    }
+    return OkStatus();
+  }
+
+ private:
+  void* pin_[2] = {nullptr, nullptr};
+  hipEvent_t ev_[2] = {nullptr, nullptr};
+};
+
+inline Status CopyToHostSync(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes < 2 * D2HStaging::kChunk) {
+    DPF_RETURN_IF_ERROR(CopyToHost(dst, src, bytes, s));
+    return HipStatus(hipStreamSynchronize(s), "sync");
+  }
+  thread_local D2HStaging staging;
+  return staging.Copy(static_cast<char*>(dst), static_cast<const char*>(src), bytes, s);
 }
 
 // Host layouts with holes (e.g. {uint32_t, uint64_t}: 16 bytes, 4 unused):
