@@ -49,8 +49,9 @@ LDS_PEAK_LOOKUPS = 256 * 32 * 2.4e9  # ds_read_b32: 32 lane-lookups/clk/CU
 AES_PER_LEAF_C5 = 4.0          # 2(2^32-1) tree + 2 * 2^32 value AES per 2^32 leaves
 # T-table lookups per c5 leaf: 2 x 160 (tree children) + 160 + 121 (the value
 # PRG pair seed, seed + 1 shares 27 lookups of rounds 1-2, and only word 0 of
-# the second value block is used: its last round is 4 lookups, not 16 —
-# DESIGN.md §3.1)
+# the second value block is used, so the compiler drops 12 of its 16
+# last-round lookups — DESIGN.md §3.1).  Measured SQ_INSTS_LDS x 64 / leaf:
+# 615 = 601 + the root-to-subtree walk (24 AES per 256-leaf subtree).
 LDS_LOOKUPS_PER_LEAF_C5 = 601
 
 
@@ -236,8 +237,27 @@ def traffic_from_profiles(kernel_substr):
             continue
         for name, e in d.items():
             if kernel_substr in name and "hbm_bytes" in e:
-                return e["hbm_bytes"], os.path.basename(f)
-    return None, None
+                return e["hbm_bytes"], os.path.basename(f), e
+    return None, None, None
+
+
+def clock_view(entry):
+    """Shader clock and LDS-array busy fraction of a kernel from its PMC
+    entry (GRBM_GUI_ACTIVE counts per XCD: / 8 XCDs / kernel time;
+    SQ_LDS_IDX_ACTIVE counts LDS-array cycles over all 256 CUs)."""
+    if not entry:
+        return None
+    c = entry.get("counters_per_launch", {})
+    ns = entry.get("avg_duration_ns")
+    if not ns or "GRBM_GUI_ACTIVE" not in c:
+        return None
+    cycles = c["GRBM_GUI_ACTIVE"] / 8.0
+    out = {"clock_ghz": cycles / ns}
+    if "SQ_LDS_IDX_ACTIVE" in c:
+        out["lds_array_busy"] = c["SQ_LDS_IDX_ACTIVE"] / 256.0 / cycles
+    if "SQ_INSTS_VALU" in c:
+        out["valu_issue_busy"] = c["SQ_INSTS_VALU"] * 2.0 / 1024.0 / cycles
+    return out
 
 
 def _cpu_worker(job):
@@ -315,6 +335,7 @@ def main():
         achieved = aes_s * OPS_PER_AES / 1e12
         lookups_s = LDS_LOOKUPS_PER_LEAF_C5 * (leaves / world) / (r["kernel_ms"] / 1e3)
         expand_traffic = traffic_from_profiles("KExpand<8, dpf_amd::EmitU32ModN64>")
+        clk = clock_view(expand_traffic[2])
         scan_traffic = traffic_from_profiles("KPirScanG<1, 4>")
         out = {
             "metric": METRIC, "value": value, "unit": "leaves/s", "n_gpus": world,
@@ -343,6 +364,11 @@ def main():
                          "aes_per_launch": aes_per_launch, "aes_per_leaf": AES_PER_LEAF_C5,
                          "aes_per_s_per_gpu": aes_s,
                          "lookups_per_leaf": LDS_LOOKUPS_PER_LEAF_C5,
+                         # the part's clock under this kernel (profile of this
+                         # build) and the fraction against the LDS peak at it
+                         "measured": (dict(clk, frac_at_measured_clock=(
+                             lookups_s / (LDS_PEAK_LOOKUPS * clk["clock_ghz"] / 2.4)))
+                             if clk else None),
                          # implementation-independent view:
                          # a bitsliced AES needs 757.5 gate ops per block
                          "valu_equivalent": {"ops_per_aes": OPS_PER_AES,

@@ -168,9 +168,8 @@ __device__ __forceinline__ void RoundCombine(const uint32_t (&t)[4][4], const K&
 // waitcnt-separated groups), then combines: per output column
 // T0[a] ^ T1[b] ^ rotl16(T0[c] ^ T1[d] ^ rotr16(rk)) = 2 v_bitop3 + 1 alignbit.
 // AesFromRound runs rounds R0..10 (the states already hold round R0-1's
-// output).  OddCols < 4: the odd states' last round produces only output
-// columns 0..OddCols-1 (4 lookups each); the other columns are left zero.
-template <int N, int R0, class K, int OddCols = 4>
+// output).
+template <int N, int R0, class K>
 __device__ __forceinline__ void AesFromRound(uint32_t (&w)[N][4], const K& key,
                                              const Lds& L) {
 #pragma unroll
@@ -191,7 +190,6 @@ __device__ __forceinline__ void AesFromRound(uint32_t (&w)[N][4], const K& key,
   for (int n = 0; n < N; ++n)
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      if ((n & 1) && c >= OddCols) continue;
       t[n][c][0] = LoadT0(L, w[n][c], 0);
       t[n][c][1] = LoadT0(L, w[n][(c + 1) & 3], 1);
       t[n][c][2] = LoadT0(L, w[n][(c + 2) & 3], 2);
@@ -201,23 +199,14 @@ __device__ __forceinline__ void AesFromRound(uint32_t (&w)[N][4], const K& key,
   __builtin_amdgcn_sched_group_barrier(0x002, 16 * N, 0);
   __builtin_amdgcn_sched_group_barrier(0x100, 16 * N, 0);
 #endif
-  uint32_t out[N][4];
 #pragma unroll
   for (int n = 0; n < N; ++n)
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      if ((n & 1) && c >= OddCols) {
-        out[n][c] = 0u;
-        continue;
-      }
       const uint32_t lo = __builtin_amdgcn_perm(t[n][c][1], t[n][c][0], 0x0c0c0501u);
       const uint32_t hi = __builtin_amdgcn_perm(t[n][c][3], t[n][c][2], 0x07020c0cu);
-      out[n][c] = key.post(n, 40 + c, Xor3(lo, hi, key.rk(n, 40 + c)));
+      w[n][c] = key.post(n, 40 + c, Xor3(lo, hi, key.rk(n, 40 + c)));
     }
-#pragma unroll
-  for (int n = 0; n < N; ++n)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) w[n][c] = out[n][c];
 }
 
 template <int N, class K>
@@ -237,9 +226,7 @@ __device__ __forceinline__ void AesN(uint32_t (&w)[N][4], const K& key,
 // (one lookup differs: T0 of byte 8); after round 2 each column differs by
 // one lookup.  So the odd block costs 1 + 4 lookups for rounds 1-2 instead
 // of 32: 133 instead of 160 lookups per odd block.  Keys: one fixed key.
-// OddCols: output columns of the odd blocks the caller uses (the rest is
-// left zero; c5 reads only word 0 of its second value block: 121 lookups).
-template <int NP, class K, int OddCols = 4>
+template <int NP, class K>
 __device__ __forceinline__ void AesPairs(uint32_t (&w)[2 * NP][4], const K& key,
                                          const Lds& L) {
   uint32_t e[NP][4], t[NP][4][4], x[NP][4];
@@ -282,7 +269,7 @@ __device__ __forceinline__ void AesPairs(uint32_t (&w)[2 * NP][4], const K& key,
 #pragma unroll
     for (int c = 0; c < 4; ++c) w[2 * p][c] = e[p][c];
   }
-  AesFromRound<2 * NP, 3, K, OddCols>(w, key, L);
+  AesFromRound<2 * NP, 3>(w, key, L);
 }
 
 // sigma(x) = (x.hi ^ x.lo, x.hi) (aes_128_fixed_key_hash.cc:75-78) in words.
@@ -556,9 +543,8 @@ struct ExpandCtx {
 
 // Value PRG of one seed: block j = H_value(seed + j) (cc:523-547).
 // kEven: every seed has bit 0 clear (a seed whose control bit was just
-// extracted), so blocks (2i, 2i+1) go through AesPairs.  OddCols: words of
-// the odd blocks the caller reads (only with kEven; the others are garbage).
-template <int NS, int BN, bool kEven = false, int OddCols = 4>
+// extracted), so blocks (2i, 2i+1) go through AesPairs.
+template <int NS, int BN, bool kEven = false>
 __device__ __forceinline__ void HashWords(const uint32_t (&x)[NS][4],
                                           uint32_t (&h)[NS][BN][4], const Lds& L) {
   uint32_t st[NS * BN][4], sg[NS * BN][4];
@@ -579,7 +565,7 @@ __device__ __forceinline__ void HashWords(const uint32_t (&x)[NS][4],
     }
   }
   if constexpr (kEven && BN % 2 == 0 && DPF_VALUE_PAIRS) {
-    AesPairs<NS * BN / 2, DpfKeyAt<2>, OddCols>(st, DpfKeyAt<2>{}, L);
+    AesPairs<NS * BN / 2>(st, DpfKeyAt<2>{}, L);
   } else {
     AesN<NS * BN>(st, DpfKeyAt<2>{}, L);
   }

@@ -37,7 +37,6 @@ namespace dpf_amd {
 template <int BN>
 struct EmitGeneric {
   static constexpr int kBN = BN;
-  static constexpr int kOddCols = 4;
   static constexpr bool kCanStage = false;
   __device__ static void Emit(const ExpandCtx& E, const uint32_t (&h)[BN][4], uint32_t t,
                               int64_t g) {
@@ -119,7 +118,6 @@ __device__ __forceinline__ void StoreLeaf16(const ExpandCtx& E, const uint4& v, 
 template <int B>
 struct EmitDirect {
   static constexpr int kBN = 1;
-  static constexpr int kOddCols = 4;
   static constexpr bool kCanStage = true;  // when Packed(vt)
   // Whole 16-byte blocks per leaf (every element of the block is returned).
   __device__ static bool Packed(const VtDev& vt) { return vt.cepb * B == 16; }
@@ -163,8 +161,6 @@ struct EmitDirect {
 // bytes[16..20); element 1 = block mod m.
 struct EmitU32ModN64 {
   static constexpr int kBN = 2;
-  // of the second value block only word 0 is read (h[1][0] below)
-  static constexpr int kOddCols = 1;
   static constexpr bool kCanStage = true;  // when Packed(vt)
   // libstdc++ tuple layout: u64 at 0, u32 at 8, stride 16.
   __device__ static bool Packed(const VtDev& vt) {
@@ -282,7 +278,7 @@ __device__ __forceinline__ void Dfs(const ExpandCtx& E, LeafStage& S, const uint
     uint32_t xs[1][4] = {{x[0], x[1], x[2], x[3]}};
     uint32_t h[1][BN][4];
     // For D > 0 the seed comes out of Expand2 with its LSB cleared.
-    HashWords<1, BN, (D > 0), Em::kOddCols>(xs, h, E.L);
+    HashWords<1, BN, (D > 0)>(xs, h, E.L);
     EmitStagedLeaf<D, Em, BN>(E, S, h[0], t, chunk, j);
   } else {
     const Cw cw = LoadCw(E.a.cw_seed, E.a.ccl, E.a.ccr, level);
