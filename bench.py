@@ -61,12 +61,22 @@ def log(*a):
 
 
 def setup():
+    """One process per GPU over RCCL.  DPF_AMD_BENCH_BACKEND=gloo rehearses
+    the N-rank data path on fewer GPUs (ranks share devices round-robin;
+    collectives through host memory) — a correctness check of the sharding,
+    not a measurement."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("DPF_AMD_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, torch.device("cuda", local)
 
 
@@ -79,7 +89,8 @@ def barrier(world):
 def max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -177,7 +188,12 @@ def bench_pir(args, world, rank, device):
     if r_lo <= idx < r_hi:
         rec_idx.copy_(db[(idx - r_lo) * rec:(idx - r_lo + 1) * rec])
     if world > 1:
-        dist.all_reduce(rec_idx, op=dist.ReduceOp.SUM)
+        if dist.get_backend() == "nccl":
+            dist.all_reduce(rec_idx, op=dist.ReduceOp.SUM)
+        else:
+            h = rec_idx.cpu().to(torch.int32)
+            dist.all_reduce(h, op=dist.ReduceOp.SUM)
+            rec_idx.copy_(h.to(torch.uint8))
     ok = bool(torch.equal(a ^ b, rec_idx))
     for _ in range(args.warmup):
         query(keys[0])

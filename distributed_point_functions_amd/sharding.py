@@ -45,9 +45,12 @@ def allgather_xor(part, world: int, fold: Callable = None):
     if world == 1:
         return part
     gathered = torch.empty(world * part.numel(), dtype=part.dtype, device=part.device)
-    dist.all_gather_into_tensor(gathered, part.contiguous().view(-1)) \
-        if part.is_cuda else dist.all_gather(list(gathered.view(world, -1).unbind(0)),
-                                             part.contiguous().view(-1))
+    if part.is_cuda and dist.get_backend() == "nccl":
+        dist.all_gather_into_tensor(gathered, part.contiguous().view(-1))
+    else:  # gloo (CPU tests; the 1-GPU multi-rank rehearsal): host buffers
+        host = torch.empty(world * part.numel(), dtype=part.dtype)
+        dist.all_gather(list(host.view(world, -1).unbind(0)), part.contiguous().view(-1).cpu())
+        gathered.copy_(host)
     out = torch.empty_like(part)
     if fold is None:
         from . import kernels
