@@ -723,6 +723,8 @@ using dpf_internal_host::DeviceBuffer;
 using dpf_internal_host::HipStatus;
 using dpf_internal_host::HostTrace;
 using dpf_internal_host::ThreadStream;
+using dpf_internal_host::ThreadUploadRing;
+using dpf_internal_host::UploadRing;
 
 namespace {
 
@@ -1390,6 +1392,40 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
   for (int64_t i = 0; i < n; ++i) {
     tree[i] = m.epb > 1 ? (evaluation_points[i] >> bbits) : evaluation_points[i];
     if (m.epb > 1) bidx[i] = static_cast<uint8_t>(evaluation_points[i] & ((uint128{1} << bbits) - 1));
+  }
+  if (ctx == nullptr) {
+    // The common call (one EvaluateAt per key): every input in one pinned
+    // slot and one DMA, inputs and outputs in one pooled allocation, the
+    // key's seed passed once (the batched kernel with one key) — per-call
+    // overhead, not the kernel, is what a caller of this API sees.
+    const uint128 seed = MakeUint128(key.seed().high(), key.seed().low());
+    const uint8_t cb = static_cast<uint8_t>(key.party() != 0);
+    const int levels = m.tree_level;
+    CwArrays cw = KeyCws(key, 0, levels);
+    using Part = UploadRing::HostPart;
+    const Part parts[6] = {{tree.data(), size_t(16) * n},
+                           {&seed, 16},
+                           {cw.seeds.data(), size_t(16) * levels},
+                           {cw.ccl.data(), size_t(levels)},
+                           {cw.ccr.data(), size_t(levels)},
+                           {&cb, 1}};
+    size_t off[6];
+    const size_t in_bytes = UploadRing::PackedLayout(parts, 6, off);
+    const size_t bi_off = in_bytes;
+    const size_t out_off = bi_off + (m.epb > 1 ? ((size_t(n) + 15) & ~size_t{15}) : 0);
+    DeviceBuffer buf;
+    DPF_RETURN_IF_ERROR(buf.Alloc(out_off + size_t(n) * vt.out_stride, s));
+    char* d = buf.as<char>();
+    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 6, in_bytes, off, s));
+    if (m.epb > 1) DPF_RETURN_IF_ERROR(ThreadUploadRing().Copy(d + bi_off, bidx.data(), n, s));
+    DPF_RETURN_IF_ERROR(ClearPadding(vt, d + out_off, n * vt.out_stride, s));
+    DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_points_batched(
+        1, n, d + off[1], reinterpret_cast<const uint8_t*>(d + off[5]), d + off[0], 0, levels,
+        d + off[2], reinterpret_cast<const uint8_t*>(d + off[3]),
+        reinterpret_cast<const uint8_t*>(d + off[4]), &vt,
+        m.epb > 1 ? reinterpret_cast<const uint8_t*>(d + bi_off) : nullptr, nullptr,
+        key.party(), nullptr, reinterpret_cast<const uint64_t*>(corr.data()), d + out_off, s)));
+    return CopyToHostSync(out, d + out_off, n * vt.out_stride, s);
   }
   DeviceBuffer seeds, cbs, paths, bi, cws, ccl, ccr, dout;
   int start_level = 0;

@@ -243,6 +243,25 @@ class UploadRing {
     }
   }
   Status Copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    const HostPart part{src, bytes};
+    return CopyPacked(dst, &part, 1, bytes, nullptr, s);
+  }
+  // Several host arrays in one slot and one DMA: part i lands at dst +
+  // off[i] (16-byte aligned; PackedLayout computes the offsets and total).
+  struct HostPart {
+    const void* p;
+    size_t bytes;
+  };
+  static size_t PackedLayout(const HostPart* parts, int k, size_t* off) {
+    size_t at = 0;
+    for (int i = 0; i < k; ++i) {
+      if (off) off[i] = at;
+      at += (parts[i].bytes + 15) & ~size_t{15};
+    }
+    return at;
+  }
+  Status CopyPacked(void* dst, const HostPart* parts, int k, size_t bytes, const size_t* off,
+                    hipStream_t s) {
     if (bytes == 0) return OkStatus();
     Slot& sl = slots_[next_];
     next_ = (next_ + 1) % kSlots;
@@ -265,7 +284,9 @@ class UploadRing {
           HipStatus(hipHostGetDevicePointer(&sl.dev, sl.host, 0), "hipHostGetDevicePointer"));
       sl.cap = cap;
     }
-    std::memcpy(sl.host, src, bytes);
+    for (int i = 0; i < k; ++i)
+      if (parts[i].bytes)
+        std::memcpy(static_cast<char*>(sl.host) + (off ? off[i] : 0), parts[i].p, parts[i].bytes);
     if (Mode() == kSdma || Mode() == kSdmaSync) {
       DPF_RETURN_IF_ERROR(
           HipStatus(hipMemcpyAsync(dst, sl.host, bytes, hipMemcpyHostToDevice, s), "upload"));
