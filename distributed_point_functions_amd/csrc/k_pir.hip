@@ -338,12 +338,6 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
 #ifndef DPF_SCAN_M4_ADDTID
 #define DPF_SCAN_M4_ADDTID 1  // row stores as ds_write_addtid_b32 (inline asm)
 #endif
-#ifndef DPF_SCAN_M4_WAIT_STORES
-#define DPF_SCAN_M4_WAIT_STORES 0  // drain the addtid stores inside their asm block
-#endif
-#ifndef DPF_SCAN_M4_DBUF
-#define DPF_SCAN_M4_DBUF 0  // diagnostics: alternate two tables per wave
-#endif
 #ifndef DPF_SCAN_M4_PREFETCH
 #define DPF_SCAN_M4_PREFETCH 1  // 4-record groups in flight per wave
 #endif
@@ -356,7 +350,7 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
 // last, partial tile reads records past num_records as zero.
 template <int P, bool FULL>
 __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint4 s,
-                                           uint32_t (&acc)[64 / P], uint32_t* t_base, int lane,
+                                           uint32_t (&acc)[64 / P], uint32_t* t, int lane,
                                            int cpart, bool col_ok, int dw_lo) {
   constexpr int CPL = 16 / P;
   constexpr int ROW = 17;
@@ -399,7 +393,6 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
     for (int i = 0; i < 4 * (PF - 1); ++i) xq[i] = xq[i + 4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) xq[4 * (PF - 1) + i] = load((4 * (k + PF) + i) & 127);
-    uint32_t* t = (DPF_SCAN_M4_DBUF && (k & 1)) ? t_base + 16 * ROW * 4 : t_base;
     const uint32_t x01 = x[0] ^ x[1], x012 = x01 ^ x[2];
     const uint32_t r[16] = {0u,          x[0],        x[1],        x01,
                             x[2],        x[0] ^ x[2], x[1] ^ x[2], x012,
@@ -424,9 +417,6 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
         "ds_write_addtid_b32 %10 offset:2992\n\tds_write_addtid_b32 %11 offset:3264\n\t"
         "ds_write_addtid_b32 %12 offset:3536\n\tds_write_addtid_b32 %13 offset:3808\n\t"
         "ds_write_addtid_b32 %14 offset:4080"
-#if DPF_SCAN_M4_WAIT_STORES
-        "\n\ts_waitcnt lgkmcnt(0)"
-#endif
         :
         : "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]),
           "v"(r[8]), "v"(r[9]), "v"(r[10]), "v"(r[11]), "v"(r[12]), "v"(r[13]), "v"(r[14]),
@@ -473,19 +463,23 @@ void KPirScanM4(ScanArgs a) {
   constexpr int QW = 64 / P;        // queries per wave
   constexpr int CPL = 16 / P;       // 16-byte columns of the slice per lane
   constexpr int ROW = 17;           // uint4 per table row (272 B)
-  __shared__ uint4 tab[kScanM4Waves][1 + DPF_SCAN_M4_DBUF][16 * ROW];
+  __shared__ uint4 tab[kScanM4Waves][16 * ROW];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t part = (int64_t)blockIdx.x * kScanM4Waves + wave;
+  // qgroups = 2 (P = 1, 65-128 queries): the waves of a pair scan the same
+  // tiles for queries [0, 64) and [64, 128), each with its own table — one
+  // pass over the rows instead of two, no barrier (the pair's second loads
+  // of a tile mostly hit in cache).
+  const int qg = a.qgroups;
+  const int64_t part = (int64_t)blockIdx.x * (kScanM4Waves / qg) + wave / qg;
   if (part >= a.parts) return;  // wave-uniform; no block barrier below
-  const int q = lane % QW, cpart = lane / QW;
+  const int q = (wave % qg) * QW + lane % QW, cpart = lane / QW;
   const int dw_lo = blockIdx.y * 64;
   const int width = min(64, a.C * 4 - dw_lo);  // dwords of this slice
   const bool col_ok = lane < width;
   const bool q_ok = q < a.nq;
-  uint32_t* t = reinterpret_cast<uint32_t*>(tab[wave][0]);
+  uint32_t* t = reinterpret_cast<uint32_t*>(tab[wave]);
   t[lane] = 0u;  // row 0 (no record selected) stays zero
-  if (DPF_SCAN_M4_DBUF) reinterpret_cast<uint32_t*>(tab[wave][DPF_SCAN_M4_DBUF])[lane] = 0u;
   uint32_t acc[4 * CPL];
 #pragma unroll
   for (int i = 0; i < 4 * CPL; ++i) acc[i] = 0u;
@@ -510,11 +504,19 @@ void KPirScanM4(ScanArgs a) {
   }
 }
 
-int PirScanM4Queries(int rem) { return std::min(rem, rem > 32 ? 64 : rem > 16 ? 32 : 16); }
+#ifndef DPF_SCAN_M4_PAIRS
+#define DPF_SCAN_M4_PAIRS 1  // wave pairs for 65-128 queries (else 64 per pass)
+#endif
+int PirScanM4Queries(int rem) {
+  return std::min(rem, (DPF_SCAN_M4_PAIRS && rem > 64) ? 128 : rem > 32 ? 64 : rem > 16 ? 32 : 16);
+}
 
-int LaunchPirScanM4(int nq, int parts, int slices, hipStream_t st, const ScanArgs& a) {
+int LaunchPirScanM4(int nq, int parts, int slices, hipStream_t st, const ScanArgs& args) {
   const int P = nq > 32 ? 1 : nq > 16 ? 2 : 4;
-  const dim3 g((parts + kScanM4Waves - 1) / kScanM4Waves, slices);
+  ScanArgs a = args;
+  a.qgroups = nq > 64 ? 2 : 1;
+  const int per_block = kScanM4Waves / a.qgroups;
+  const dim3 g((parts + per_block - 1) / per_block, slices);
   if (P == 1)
     hipLaunchKernelGGL((KPirScanM4<1>), g, dim3(kScanM4Block), 0, st, a);
   else if (P == 2)

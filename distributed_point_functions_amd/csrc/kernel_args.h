@@ -117,6 +117,8 @@ struct ScanArgs {
   int32_t nq;           // queries in this pass (<= QN)
   int32_t total_q;
   int32_t parts;        // partials written per query (KPirScanM4: waves in use)
+  int32_t qgroups;      // KPirScanM4: waves scanning the same tiles (1 or 2)
+  int32_t pad;
 };
 
 // KPirScanM4: 4 independent waves per block, one LDS table pair per wave.

@@ -473,6 +473,8 @@ int dpf_amd_inner_product(const void* db, int64_t num_records, int64_t record_st
   a.C = C;
   a.total_q = num_queries;
   a.parts = grid;
+  a.qgroups = 1;
+  a.pad = 0;
   const dim3 g(grid, (C + 63) / 64);
   for (int q0 = 0; q0 < num_queries;) {
     const int rem = num_queries - q0;
