@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <array>
 #include <cmath>
 #include <cstdio>
@@ -1067,16 +1068,19 @@ namespace {
 // ComputePartialEvaluations (cc:374-476): selects the stored partial
 // evaluations for `prefixes` (host map, as the reference's btree), walks them
 // on the device to `hierarchy_level`'s tree level, and rewrites ctx.
-// Returns device seeds / control bits for the prefixes.
+// Returns device seeds / control bits for the prefixes, inside `buf`: every
+// input of the walk goes up in one pinned slot and one DMA (c3: 2^16
+// prefixes per level, where host work rivals the kernels).
 Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixes,
                                  int hierarchy_level, bool update_ctx, EvaluationContext& ctx,
-                                 hipStream_t s, DeviceBuffer* seeds_dev, DeviceBuffer* cb_dev) {
+                                 hipStream_t s, DeviceBuffer* buf, void** seeds_dev,
+                                 uint8_t** cb_dev) {
   HostTrace trace("PartialEvaluations");
   const int64_t n = static_cast<int64_t>(prefixes.size());
   int start_level = st.hierarchy_to_tree[ctx.partial_evaluations_level()];
   const int stop_level = st.hierarchy_to_tree[hierarchy_level];
-  std::vector<uint128> seeds(n);
-  std::vector<uint8_t> cbs(n);
+  std::unique_ptr<uint128[]> seeds(new uint128[n > 0 ? n : 1]);
+  std::unique_ptr<uint8_t[]> cbs(new uint8_t[n > 0 ? n : 1]);
   if (ctx.partial_evaluations_size() > 0 && start_level <= stop_level) {
     const int shift = stop_level - start_level;
     const auto& pes = ctx.partial_evaluations();
@@ -1087,23 +1091,39 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
     auto query = [&](int64_t i) { return shift < 128 ? (prefixes[i] >> shift) : uint128{0}; };
     // Sorted fast path (the common case: prefixes come from a sorted
     // candidate list, and the stored evaluations are the previous call's
-    // sorted tree indices): a merge join instead of the reference's btree.
-    bool sorted = true;
-    for (int64_t j = 1; j < m && sorted; ++j) sorted = pe_prefix(j - 1) < pe_prefix(j);
-    for (int64_t i = 1; i < n && sorted; ++i) sorted = query(i - 1) <= query(i);
-    if (sorted) {
+    // sorted tree indices): one merge-join pass instead of the reference's
+    // btree, checking both orders on the way.  Anything it cannot decide
+    // (an unsorted side, a prefix it does not find) goes to the hash path,
+    // which also produces the reference's errors.
+    bool merged = m > 0;
+    {
       int64_t j = 0;
-      for (int64_t i = 0; i < n; ++i) {
-        const uint128 pp = query(i);
-        while (j < m && pe_prefix(j) < pp) ++j;
-        if (j == m || pe_prefix(j) != pp)
-          return InvalidArgumentError(
-              "Prefix not present in ctx.partial_evaluations at hierarchy level " +
-              std::to_string(hierarchy_level));
+      uint128 pj = m > 0 ? pe_prefix(0) : 0, prev_q = 0;
+      for (int64_t i = 0; i < n && merged; ++i) {
+        const uint128 q = query(i);
+        if (i > 0 && q < prev_q) {
+          merged = false;
+          break;
+        }
+        prev_q = q;
+        while (pj < q) {
+          if (++j == m) break;
+          const uint128 next = pe_prefix(j);
+          if (next <= pj) {
+            merged = false;
+            break;
+          }
+          pj = next;
+        }
+        if (!merged || j == m || pj != q) {
+          merged = false;
+          break;
+        }
         seeds[i] = MakeUint128(pes[j].seed().high(), pes[j].seed().low());
         cbs[i] = pes[j].control_bit() ? 1 : 0;
       }
-    } else {
+    }
+    if (!merged) {
       std::unordered_map<uint128, std::pair<uint128, bool>, U128Hash> prev;
       prev.reserve(m * 2);
       for (const PartialEvaluation& e : pes) {
@@ -1128,32 +1148,40 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
     }
   } else {
     const uint128 seed = MakeUint128(ctx.key().seed().high(), ctx.key().seed().low());
-    std::fill(seeds.begin(), seeds.end(), seed);
-    std::fill(cbs.begin(), cbs.end(), static_cast<uint8_t>(ctx.key().party() != 0));
+    std::fill(seeds.get(), seeds.get() + n, seed);
+    std::fill(cbs.get(), cbs.get() + n, static_cast<uint8_t>(ctx.key().party() != 0));
     start_level = 0;
   }
   trace.Mark("lookup");
   const int levels = stop_level - start_level;
   CwArrays cw = KeyCws(ctx.key(), start_level, stop_level);
-  DeviceBuffer paths, cws, ccl, ccr;
-  DPF_RETURN_IF_ERROR(seeds_dev->Upload(seeds.data(), 16 * n, s));
-  DPF_RETURN_IF_ERROR(cb_dev->Upload(cbs.data(), n, s));
-  if (levels > 0 && n > 0) {
-    DPF_RETURN_IF_ERROR(paths.Upload(prefixes.data(), 16 * n, s));
-    DPF_RETURN_IF_ERROR(cws.Upload(cw.seeds.data(), 16 * levels, s));
-    DPF_RETURN_IF_ERROR(ccl.Upload(cw.ccl.data(), levels, s));
-    DPF_RETURN_IF_ERROR(ccr.Upload(cw.ccr.data(), levels, s));
+  const bool walk = levels > 0 && n > 0;
+  using Part = UploadRing::HostPart;
+  const Part parts[6] = {{seeds.get(), size_t(16) * n},
+                         {cbs.get(), size_t(n)},
+                         {prefixes.data(), walk ? size_t(16) * n : 0},
+                         {cw.seeds.data(), walk ? size_t(16) * levels : 0},
+                         {cw.ccl.data(), walk ? size_t(levels) : 0},
+                         {cw.ccr.data(), walk ? size_t(levels) : 0}};
+  size_t off[6];
+  const size_t bytes = UploadRing::PackedLayout(parts, 6, off);
+  DPF_RETURN_IF_ERROR(buf->Alloc(bytes, s));
+  char* d = buf->as<char>();
+  DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 6, bytes, off, s));
+  *seeds_dev = d + off[0];
+  *cb_dev = reinterpret_cast<uint8_t*>(d + off[1]);
+  if (walk) {
     DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_seeds(
-        n, levels, levels, seeds_dev->get(), cb_dev->as<uint8_t>(), paths.get(), 0, cws.get(),
-        ccl.as<uint8_t>(), ccr.as<uint8_t>(), dpf_amd::kPrgKeyLeftLo, dpf_amd::kPrgKeyLeftHi,
-        dpf_amd::kPrgKeyRightLo, dpf_amd::kPrgKeyRightHi, seeds_dev->get(),
-        cb_dev->as<uint8_t>(), s)));
+        n, levels, levels, d + off[0], *cb_dev, d + off[2], 0, d + off[3],
+        reinterpret_cast<const uint8_t*>(d + off[4]), reinterpret_cast<const uint8_t*>(d + off[5]),
+        dpf_amd::kPrgKeyLeftLo, dpf_amd::kPrgKeyLeftHi, dpf_amd::kPrgKeyRightLo,
+        dpf_amd::kPrgKeyRightHi, d + off[0], *cb_dev, s)));
   }
   trace.Mark("upload+walk_launch");
   ctx.clear_partial_evaluations();
   if (update_ctx && n > 0) {
-    DPF_RETURN_IF_ERROR(CopyToHost(seeds.data(), seeds_dev->get(), 16 * n, s));
-    DPF_RETURN_IF_ERROR(CopyToHost(cbs.data(), cb_dev->get(), n, s));
+    DPF_RETURN_IF_ERROR(CopyToHost(seeds.get(), *seeds_dev, 16 * n, s));
+    DPF_RETURN_IF_ERROR(CopyToHost(cbs.get(), *cb_dev, n, s));
     DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
     std::vector<PartialEvaluation>* pe = ctx.mutable_partial_evaluations();
     pe->resize(n);
@@ -1254,18 +1282,25 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
 
   trace.Mark("checks+dedup");
   // ExpandAndUpdateContext (cc:478-521): roots on the device.
-  DeviceBuffer root_seeds, root_cb;
+  DeviceBuffer roots;
+  void* root_seeds = nullptr;
+  uint8_t* root_cb = nullptr;
   int start_level = 0;
   if (prefixes.empty()) {
     const uint128 seed = MakeUint128(ctx.key().seed().high(), ctx.key().seed().low());
     const uint8_t cb = static_cast<uint8_t>(ctx.key().party() != 0);
-    DPF_RETURN_IF_ERROR(root_seeds.Upload(&seed, 16, s));
-    DPF_RETURN_IF_ERROR(root_cb.Upload(&cb, 1, s));
+    const UploadRing::HostPart parts[2] = {{&seed, 16}, {&cb, 1}};
+    size_t off[2];
+    const size_t bytes = UploadRing::PackedLayout(parts, 2, off);
+    DPF_RETURN_IF_ERROR(roots.Alloc(bytes, s));
+    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(roots.get(), parts, 2, bytes, off, s));
+    root_seeds = roots.as<char>() + off[0];
+    root_cb = reinterpret_cast<uint8_t*>(roots.as<char>() + off[1]);
   } else {
     const bool update_ctx = hierarchy_level < L - 1;
     DPF_RETURN_IF_ERROR(ComputePartialEvaluations(
         st, Span<const uint128>(tree_indices.data(), tree_indices.size()), prev_h, update_ctx,
-        ctx, s, &root_seeds, &root_cb));
+        ctx, s, &roots, &root_seeds, &root_cb));
     start_level = st.hierarchy_to_tree[prev_h];
   }
   trace.Mark("partial_evaluations");
@@ -1294,7 +1329,7 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   }
   DPF_RETURN_IF_ERROR(ClearPadding(vt, expand_out, expanded * stride, s));
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_expand_and_correct(
-      num_roots, root_seeds.get(), root_cb.as<uint8_t>(), levels, cws.get(), ccl.as<uint8_t>(),
+      num_roots, root_seeds, root_cb, levels, cws.get(), ccl.as<uint8_t>(),
       ccr.as<uint8_t>(), &vt, reinterpret_cast<const uint64_t*>(corr.data()),
       ctx.key().party(), cepb, 0, num_roots << levels, expand_out, s)));
 
@@ -1427,18 +1462,15 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
         key.party(), nullptr, reinterpret_cast<const uint64_t*>(corr.data()), d + out_off, s)));
     return CopyToHostSync(out, d + out_off, n * vt.out_stride, s);
   }
-  DeviceBuffer seeds, cbs, paths, bi, cws, ccl, ccr, dout;
-  int start_level = 0;
-  if (ctx == nullptr) {
-    std::vector<uint128> sv(n, MakeUint128(key.seed().high(), key.seed().low()));
-    std::vector<uint8_t> cv(n, static_cast<uint8_t>(key.party() != 0));
-    DPF_RETURN_IF_ERROR(seeds.Upload(sv.data(), 16 * n, s));
-    DPF_RETURN_IF_ERROR(cbs.Upload(cv.data(), n, s));
-  } else {
-    DPF_RETURN_IF_ERROR(ComputePartialEvaluations(st, Span<const uint128>(tree.data(), n),
-                                                  hierarchy_level, true, *ctx, s, &seeds, &cbs));
-    start_level = m.tree_level;
-  }
+  // With a context: the stored partial evaluations are walked to this
+  // level's tree level first (EvaluateAt h:349-378 with ctx).
+  DeviceBuffer pe, paths, bi, cws, ccl, ccr, dout;
+  void* seeds = nullptr;
+  uint8_t* cbs = nullptr;
+  DPF_RETURN_IF_ERROR(ComputePartialEvaluations(st, Span<const uint128>(tree.data(), n),
+                                                hierarchy_level, true, *ctx, s, &pe, &seeds,
+                                                &cbs));
+  const int start_level = m.tree_level;
   const int levels = m.tree_level - start_level;
   CwArrays cw = KeyCws(key, start_level, m.tree_level);
   DPF_RETURN_IF_ERROR(paths.Upload(tree.data(), 16 * n, s));
@@ -1449,7 +1481,7 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
   DPF_RETURN_IF_ERROR(dout.Alloc(n * vt.out_stride, s));
   DPF_RETURN_IF_ERROR(ClearPadding(vt, dout.get(), n * vt.out_stride, s));
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_points(
-      n, seeds.get(), cbs.as<uint8_t>(), paths.get(), 0, levels, levels, cws.get(),
+      n, seeds, cbs, paths.get(), 0, levels, levels, cws.get(),
       ccl.as<uint8_t>(), ccr.as<uint8_t>(), &vt, bi.as<uint8_t>(), nullptr, key.party(), nullptr,
       reinterpret_cast<const uint64_t*>(corr.data()), dout.get(), nullptr, nullptr, s)));
   DPF_RETURN_IF_ERROR(CopyToHostSync(out, dout.get(), n * vt.out_stride, s));

@@ -140,7 +140,14 @@ def c2(dev, reps):
            for k in range(nkeys)]
     out = torch.empty(nkeys * per * 16, dtype=torch.uint8, device=dev)
 
-    def tier1():
+    if C2_BATCHED_ONLY:  # profiling the batched kernel alone
+        def tier1():
+            pass
+    else:
+        def tier1():
+            _tier1()
+
+    def _tier1():
         for k in range(nkeys):
             kernels.evaluate_points(seeds[k], cbs[k], pts[k], 0, L, kd[k]["cw"], kd[k]["ccl"],
                                     kd[k]["ccr"], desc, party_all=kd[k]["party"],
@@ -169,6 +176,8 @@ def c2(dev, reps):
                     "tier1_multi_key_points_per_s": nkeys * per / tm,
                     "tier1_multi_key_lds_frac": lds_frac(nkeys * per * (L + 1) / tm)})
         got = out.view(torch.int64).view(-1, 2).cpu().numpy().view(np.uint64)
+    if C2_BATCHED_ONLY:
+        return res
     plist = [kernels.tensor_u128(p) for p in pts]
 
     def tier2():
@@ -259,6 +268,7 @@ def c3(dev, reps):
 
 C4Q_QUERIES = (1, 8, 16, 32, 64, 100)
 C4Q_AB = True
+C2_BATCHED_ONLY = False
 
 
 def c4q(dev, reps):
@@ -462,8 +472,10 @@ def main():
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--c4q-queries", default=None, help="comma list, e.g. 64 (profiling)")
     ap.add_argument("--no-ab", action="store_true", help="c4q: skip the kernel A/B")
+    ap.add_argument("--c2-batched-only", action="store_true", help="c2: the batched kernel only")
     args = ap.parse_args()
-    global C4Q_QUERIES, C4Q_AB
+    global C4Q_QUERIES, C4Q_AB, C2_BATCHED_ONLY
+    C2_BATCHED_ONLY = args.c2_batched_only
     if args.c4q_queries:
         C4Q_QUERIES = tuple(int(x) for x in args.c4q_queries.split(","))
     C4Q_AB = not args.no_ab

@@ -1,11 +1,12 @@
 #!/bin/bash
-# rocprofv3 of the many-query scan alone (c4: 2^26 x 256 B, Q = 64):
+# rocprofv3 of tools/bench_configs.py runs (default: the many-query scan alone,
+# c4 2^26 x 256 B, Q = 64; ARGS=... for another config):
 # trace pass, then one PMC pass per counter group.
 TAG=${1:-r02}
 export TMPDIR=/tmp
-OUT=gpurun_out/prof_${TAG}_c4q
+OUT=gpurun_out/prof_${TAG}
 mkdir -p $OUT
-ARGS="--only c4q --c4q-queries 64 --no-ab --reps 3"
+ARGS=${ARGS:-"--only c4q --c4q-queries 64 --no-ab --reps 3"}
 run() {
   local name=$1 to=$2; shift 2
   timeout -k 10 $to rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 tools/bench_configs.py $ARGS > $OUT/$name.log 2>&1
