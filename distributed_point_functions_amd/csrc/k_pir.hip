@@ -345,10 +345,14 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
 #define DPF_SCAN_M4_READ_BATCH 16  // ds_read_b128 issued back to back
 #endif
 
-// One 128-record tile.  FULL tiles read the records through a buffer
-// resource based at the tile (record offsets in SGPRs, nontemporal); the
-// last, partial tile reads records past num_records as zero.
-template <int P, bool FULL>
+// One 128-record tile, its records read through a buffer resource based at
+// the tile (nontemporal).  The record offset goes in voffset, which the
+// range check covers: the last, partial tile limits the range to the bytes
+// left after `base`, so records past num_records read as zero, and lanes
+// past the slice's width use an offset beyond any range.  (One code path for
+// full and partial tiles: two inlined copies made the compiler keep two
+// copies of the accumulators, 163 VGPRs instead of ~100.)
+template <int P>
 __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint4 s,
                                            uint32_t (&acc)[64 / P], uint32_t* t, int lane,
                                            int cpart, bool col_ok, int dw_lo) {
@@ -356,23 +360,16 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
   constexpr int ROW = 17;
   const int rec_dwords = a.C * 4;
   const int64_t rec0 = tile << 7;
+  const bool full = rec0 + 128 <= a.num_records;
   const uint32_t* base = reinterpret_cast<const uint32_t*>(a.db) + rec0 * rec_dwords + dw_lo;
-  // The last, partial tile limits the range to the bytes left after `base`
-  // and puts the record offset in voffset, which the range check covers:
-  // records past num_records read as zero.
   const int64_t left = (a.num_records - rec0) * rec_dwords * 4 - dw_lo * 4;
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)base, 0, FULL ? 0x7fffffff : (int)left, 0x00020000);
-  // lanes past the slice's width read beyond num_records (<= 0x7fffffff): zero.
-  // Record offsets stay below 128 * rec_bytes <= 2^27 (see ScanM4Parts).
+      (void*)base, 0, full ? 0x7fffffff : (int)left, 0x00020000);
+  // record offsets stay below 128 * rec_bytes <= 2^27 (see UseScanM4)
   const int voff = col_ok ? lane * 4 : (int)0x80000000u;
+  const int rec_bytes = rec_dwords * 4;
   auto load = [&](int r) -> uint32_t {
-    if constexpr (FULL) {
-      return __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, r * rec_dwords * 4, 2);
-    } else {
-      return __builtin_amdgcn_raw_buffer_load_b32(
-          rsrc, col_ok ? r * rec_dwords * 4 + lane * 4 : (int)0x80000000u, 0, 2);
-    }
+    return __builtin_amdgcn_raw_buffer_load_b32(rsrc, col_ok ? voff + r * rec_bytes : voff, 0, 2);
   };
   // records of the next PF groups in flight (a rotating register queue);
   // the last groups re-read the tile's first, cached, records rather than
@@ -455,7 +452,7 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
 }
 
 #ifndef DPF_SCAN_M4_P1_WAVES
-#define DPF_SCAN_M4_P1_WAVES 3  // 163 VGPRs with the addtid stores
+#define DPF_SCAN_M4_P1_WAVES 5  // <= 102 VGPRs, no spill (Q = 64: 4.31 vs 4.36 ms at 4)
 #endif
 template <int P>
 __global__ __launch_bounds__(kScanM4Block, P == 1 ? DPF_SCAN_M4_P1_WAVES : P == 2 ? 4 : 6)
@@ -487,10 +484,7 @@ void KPirScanM4(ScanArgs a) {
   for (int64_t tile = part; tile < tiles; tile += a.parts) {
     const uint4 s = q_ok ? a.sel[(int64_t)(a.q0 + q) * a.sel_blocks + tile]
                          : make_uint4(0, 0, 0, 0);
-    if ((tile << 7) + 128 <= a.num_records)
-      ScanM4Tile<P, true>(a, tile, s, acc, t, lane, cpart, col_ok, dw_lo);
-    else
-      ScanM4Tile<P, false>(a, tile, s, acc, t, lane, cpart, col_ok, dw_lo);
+    ScanM4Tile<P>(a, tile, s, acc, t, lane, cpart, col_ok, dw_lo);
   }
   if (!q_ok) return;
   // this lane's columns [cpart * CPL, +CPL) of the slice, clipped to the record
