@@ -452,7 +452,7 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
 }
 
 #ifndef DPF_SCAN_M4_P1_WAVES
-#define DPF_SCAN_M4_P1_WAVES 5  // <= 102 VGPRs, no spill (Q = 64: 4.31 vs 4.36 ms at 4)
+#define DPF_SCAN_M4_P1_WAVES 4  // 100 VGPRs (5 waves: 4 spilled, Q = 64 4.31 vs 4.36 ms)
 #endif
 template <int P>
 __global__ __launch_bounds__(kScanM4Block, P == 1 ? DPF_SCAN_M4_P1_WAVES : P == 2 ? 4 : 6)
