@@ -333,3 +333,53 @@ def test_pir_leader_requires_while_waiting(api):
     assert e.value.code == 9
     assert e.value.message == ("HandleRequest: `while_waiting` was not called from `sender` "
                                "passed at construction.")
+
+
+def test_incremental_unsorted_duplicate_and_missing_prefixes(api):
+    """The partial-evaluation lookup's paths: sorted prefixes take the
+    one-pass merge join, shuffled / repeated ones the hash path (reference
+    btree semantics: outputs in the caller's order, duplicates repeated), and
+    a prefix whose parent was never evaluated fails with the reference's
+    message — all checked against the oracle."""
+    D, V, _ = api
+    spec = ("int", 64)
+    lds = [8, 16, 24]
+    levels = [(ld, spec, 40 + ld) for ld in lds]
+    rng = random.Random(77)
+    alpha = rng.getrandbits(24)
+    betas = [rng.getrandbits(64) for _ in lds]
+    seeds = (rng.getrandbits(128), rng.getrandbits(128))
+    dpf = _make(api, levels)
+    od = po.Dpf(levels)
+    k0, _ = dpf.generate_keys_incremental(alpha, betas, seeds=seeds)
+    ok0, _ = od.generate_keys(alpha, betas, seeds=seeds)
+    vt = V.from_spec(spec)
+    for order in ("sorted", "shuffled"):
+        ctx = dpf.create_evaluation_context(k0)
+        octx = od.create_evaluation_context(ok0)
+        assert vt.decode_flat(dpf.evaluate_next([], ctx, raw=True)) == od.evaluate_until(0, [], octx)
+        p1 = sorted(set(rng.sample(range(256), 40)) | {alpha >> 16})
+        if order == "shuffled":
+            p1 = p1 + p1[:5]  # duplicates
+            rng.shuffle(p1)
+        got = vt.decode_flat(dpf.evaluate_next(p1, ctx, raw=True))
+        assert got == od.evaluate_until(1, p1, octx), order
+        base = sorted(set(p1))
+        p2 = sorted({(p << 8) | rng.randrange(256) for p in base for _ in range(3)})
+        if order == "shuffled":
+            rng.shuffle(p2)
+        got = vt.decode_flat(dpf.evaluate_next(p2, ctx, raw=True))
+        assert got == od.evaluate_until(2, p2, octx), order
+    # a level-1 prefix whose level-0 parent was not among the evaluated ones
+    ctx = dpf.create_evaluation_context(k0)
+    octx = od.create_evaluation_context(ok0)
+    dpf.evaluate_next([], ctx, raw=True)
+    od.evaluate_until(0, [], octx)
+    dpf.evaluate_next([1, 2, 3], ctx, raw=True)
+    od.evaluate_until(1, [1, 2, 3], octx)
+    with pytest.raises(Exception) as ours:
+        dpf.evaluate_next([(7 << 8) | 1], ctx, raw=True)
+    with pytest.raises(Exception) as ref:
+        od.evaluate_until(2, [(7 << 8) | 1], octx)
+    assert "Prefix not present in ctx.partial_evaluations" in str(ours.value)
+    assert str(ours.value).split(":")[-1].strip() == str(ref.value).split(":")[-1].strip()
