@@ -240,8 +240,14 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
     D = 2;
   else
     D = num_levels;
-  // For small problems prefer more threads over deep DFS.
-  while (D > 2 && ((leaf_end - leaf_begin) >> D) < 65536) D = (D == 8) ? 4 : 2;
+  // For small problems prefer more threads over deep DFS.  A D = 8 thread
+  // expands 256 leaves in sequence (~1.3 ms however small the launch), so
+  // D = 8 needs 2^17 threads to beat D = 4 (tools/c1_depth_sweep.py, uint64:
+  // 2^24 tree leaves D = 8 1.32 ms vs D = 4 0.80; 2^25: 1.33 vs 1.46), and
+  // D = 4 needs 2^16 (2^19 tree leaves: D = 2 0.059 ms vs D = 4 0.112).
+  const int64_t range = leaf_end - leaf_begin;
+  if (D == 8 && (range >> 8) < (int64_t{1} << 17)) D = 4;
+  if (D == 4 && (range >> 4) < (int64_t{1} << 16)) D = 2;
   const int forced = g_expand_depth.load(std::memory_order_relaxed);
   if (forced > 0 && forced <= num_levels) D = forced;
   ExpandArgs a;

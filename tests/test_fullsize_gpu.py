@@ -2,12 +2,12 @@
 of the benchmarked configuration at its full size.
 
 `dpf_amd_expand_and_correct` picks the register-DFS depth D of KExpand<D>
-from the launch size (kernels_capi.cc): D = 8 once a launch covers >= 2^24
+from the launch size (kernels_capi.cc): D = 8 once a launch covers >= 2^25
 tree leaves, D = 4 from 2^20.  These tests
   * force D in {1, 2, 4, 8} (dpf_amd_set_expand_depth) on small domains and
     compare every output of every value type with the oracle;
-  * run the automatic choice at sizes where it picks D = 4 (2^20 tree
-    leaves) and D = 8 (2^24) and compare every output with the oracle;
+  * run the automatic choice at sizes where it picks D = 4 (2^20 and 2^24
+    tree leaves) and D = 8 (2^25) and compare every output with the oracle;
   * run the c5 bench configuration itself (log_domain_size 32,
     Tuple<uint32, IntModN<uint64, 2^64-59>>, the KExpand<8, EmitU32ModN64>
     launch the bench times) for both parties: the share sum over all 2^32
@@ -126,10 +126,10 @@ def test_forced_depth_knob_validates():
 # The automatic choice at the sizes where it selects D = 4 and D = 8
 # ---------------------------------------------------------------------------
 
-AUTO = [  # (spec, log_domain) -> tree levels L; D = 4 at L = 20, D = 8 at L = 24
-    (C5, 20), (C5, 24),
-    (("int", 64), 21), (("int", 64), 25),
-    (("xor", 128), 20), (("xor", 128), 24),
+AUTO = [  # (spec, log_domain) -> tree levels L; D = 4 at L = 20 / 24, D = 8 at L = 25
+    (C5, 20), (C5, 25),
+    (("int", 64), 21), (("int", 64), 25), (("int", 64), 26),
+    (("xor", 128), 20), (("xor", 128), 25),
 ]
 
 
@@ -138,7 +138,7 @@ def test_production_depth_full_domain_matches_oracle(K, cuda, spec, ld):
     import torch
     d, k0, k1, alpha, beta = _keys(spec, ld, seed=11)
     L = d.hierarchy_to_tree(0)
-    assert L in (20, 24)
+    assert L in (20, 24, 25)
     for key in (k0, k1):
         want = d.evaluate_until_words(0, [], d.create_evaluation_context(key))
         got = _expand(K, cuda, d, key, spec).cpu().numpy()
