@@ -205,21 +205,39 @@ __device__ __forceinline__ void PointsIter(const PointsArgs& a, const VtDev& vt,
   }
 }
 
+// KEvaluatePoints<BN> for BN <= 2 runs one point chain per lane at 8
+// waves/SIMD (1024-thread blocks, 52-57 VGPRs): c2 1.67 -> 1.57 ms against
+// two chains per lane at 4 waves/SIMD (a kernel holding both paths needs
+// 104 VGPRs); one chain at 6 waves was slower (1.74).  BN = 4 (94 VGPRs for
+// one chain) keeps two chains per lane at 4 waves.
 template <int BN>
-__global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluatePoints(PointsArgs a,
-                                                                               VtDev vt) {
+constexpr bool kPointsTwoChains = BN > 2;
+template <int BN>
+constexpr int kPointsBlockOf = kPointsTwoChains<BN> ? kPointsBlock : 1024;
+template <int BN>
+constexpr int kPointsWavesOf = kPointsTwoChains<BN> ? kPointsWaves : 8;
+
+template <int BN>
+__global__ __launch_bounds__(kPointsBlockOf<BN>, kPointsWavesOf<BN>) void KEvaluatePoints(
+    PointsArgs a, VtDev vt) {
   __shared__ uint32_t tab[kTabWords];
   FillTables(tab);
   __syncthreads();
   const Lds L = MakeLds(tab);
   const int64_t T = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; base < a.w.num_seeds;
-       base += 2 * T) {
-    if (__ballot(base + T < a.w.num_seeds) != 0) {
-      PointsIter<2, BN>(a, vt, L, base, T);
-    } else {
-      PointsIter<1, BN>(a, vt, L, base, T);
+  if constexpr (kPointsTwoChains<BN>) {
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; base < a.w.num_seeds;
+         base += 2 * T) {
+      if (__ballot(base + T < a.w.num_seeds) != 0) {
+        PointsIter<2, BN>(a, vt, L, base, T);
+      } else {
+        PointsIter<1, BN>(a, vt, L, base, T);
+      }
     }
+  } else {
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; base < a.w.num_seeds;
+         base += T)
+      PointsIter<1, BN>(a, vt, L, base, T);
   }
 }
 
@@ -233,10 +251,10 @@ __global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluatePoints(Po
 // Threads per block for a walk over n points: full blocks once the launch
 // fills every CU (two blocks each), smaller ones before that so that small
 // launches still spread over all CUs.
-static int WalkBlock(int64_t n) {
+static int WalkBlock(int64_t n, int max_block = kPointsBlock) {
   int64_t per = (n + 2 * 256 - 1) / (2 * 256);
   per = (per + 63) / 64 * 64;
-  return (int)std::min<int64_t>(kPointsBlock, std::max<int64_t>(64, per));
+  return (int)std::min<int64_t>(max_block, std::max<int64_t>(64, per));
 }
 
 // Little-endian load of an `nbytes` scalar.
@@ -343,19 +361,24 @@ int LaunchEvaluateSeeds(int64_t n, hipStream_t st, const WalkArgs& a, const KeyP
   return LaunchCheck("evaluate_seeds kernel launch");
 }
 
+template <int BN>
+static void LaunchPoints(int64_t n, hipStream_t st, const PointsArgs& a, const VtDev& vt) {
+  const int block = WalkBlock(n, kPointsBlockOf<BN>);
+  const int grid = (int)std::min<int64_t>(DPF_WALK_MAX_GRID, (n + block - 1) / block);
+  hipLaunchKernelGGL((KEvaluatePoints<BN>), dim3(grid), dim3(block), 0, st, a, vt);
+}
+
 int LaunchEvaluatePoints(int bn, int64_t n, hipStream_t st, const PointsArgs& a,
                          const VtDev& vt) {
-  const int block = WalkBlock(n);
-  const int grid = (int)std::min<int64_t>(DPF_WALK_MAX_GRID, (n + block - 1) / block);
   switch (bn) {
     case 1:
-      hipLaunchKernelGGL((KEvaluatePoints<1>), dim3(grid), dim3(block), 0, st, a, vt);
+      LaunchPoints<1>(n, st, a, vt);
       break;
     case 2:
-      hipLaunchKernelGGL((KEvaluatePoints<2>), dim3(grid), dim3(block), 0, st, a, vt);
+      LaunchPoints<2>(n, st, a, vt);
       break;
     default:
-      hipLaunchKernelGGL((KEvaluatePoints<4>), dim3(grid), dim3(block), 0, st, a, vt);
+      LaunchPoints<4>(n, st, a, vt);
   }
   return LaunchCheck("evaluate_points kernel launch");
 }
