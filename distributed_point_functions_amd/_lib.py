@@ -88,6 +88,7 @@ def lib():
     _sig(L, "dpf_amd_last_error", ctypes.c_char_p)
     _sig(L, "dpf_amd_version", ctypes.c_char_p)
     _sig(L, "dpf_amd_device_count", I32, ctypes.POINTER(ctypes.c_int))
+    _sig(L, "dpf_amd_release_cached_memory", I32, ctypes.POINTER(I64))
     _sig(L, "dpf_amd_free", None, P)
     _sig(L, "dpf_amd_aes128_mmo", I32, U64, U64, P, P, I64, P)
     _sig(L, "dpf_amd_evaluate_seeds", I32, I64, I32, I64, P, P, P, I32, P, P, P,

@@ -12,6 +12,7 @@
 #include "dpf_amd/cuckoo_hashing_sparse_dpf_pir_server.h"
 #include "dpf_amd/dense_dpf_pir_server.h"
 #include "dpf_amd/distributed_comparison_function.h"
+#include "host_device.h"
 #include "dpf_amd/distributed_point_function.h"
 #include "internal.h"
 
@@ -382,6 +383,14 @@ int dpf_amd_pir_db_build(dpf_amd_pir_db* db) {
 }
 
 void dpf_amd_pir_db_destroy(dpf_amd_pir_db* db) { delete db; }
+
+int dpf_amd_release_cached_memory(int64_t* released) {
+  auto& pool = dpf_internal_host::DevicePool::Get();
+  const size_t before = pool.cached_bytes();
+  pool.Release();
+  if (released) *released = static_cast<int64_t>(before - pool.cached_bytes());
+  return DPF_AMD_OK;
+}
 
 int64_t dpf_amd_pir_db_size(const dpf_amd_pir_db* db) {
   return db->built ? static_cast<int64_t>(db->built->size()) : 0;

@@ -1122,6 +1122,15 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
         seeds[i] = MakeUint128(pes[j].seed().high(), pes[j].seed().low());
         cbs[i] = pes[j].control_bit() ? 1 : 0;
       }
+      // The reference rejects a mismatching duplicate anywhere in the
+      // stored list (cc:390-405), not only where the queries reach: the
+      // merge result stands only if the rest of the list is strictly
+      // increasing too (then it holds no duplicate at all).
+      for (int64_t k = j + 1; k < m && merged; ++k) {
+        const uint128 next = pe_prefix(k);
+        if (next <= pj) merged = false;
+        pj = next;
+      }
     }
     if (!merged) {
       std::unordered_map<uint128, std::pair<uint128, bool>, U128Hash> prev;

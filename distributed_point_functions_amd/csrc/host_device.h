@@ -85,6 +85,23 @@ inline Status CopyToHost(void* dst, const void* src, size_t bytes, hipStream_t s
   return HipStatus(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s), "d2h");
 }
 
+// Drains `s` when it goes out of scope unless dismissed: an early error
+// return must not leave an async D2H copy in flight into host memory the
+// returning function owns (locals, unique_ptr arrays).
+class StreamSyncGuard {
+ public:
+  explicit StreamSyncGuard(hipStream_t s) : s_(s) {}
+  StreamSyncGuard(const StreamSyncGuard&) = delete;
+  StreamSyncGuard& operator=(const StreamSyncGuard&) = delete;
+  ~StreamSyncGuard() {
+    if (s_) (void)hipStreamSynchronize(s_);
+  }
+  void Dismiss() { s_ = nullptr; }
+
+ private:
+  hipStream_t s_;
+};
+
 // Host memcpy split over a few persistent worker threads: one thread copies
 // from pinned into pageable memory at ~8 GB/s, below the PCIe DMA rate.
 class MemcpyPool {
@@ -227,7 +244,11 @@ inline Status ClearPadding(const dpf_amd_value_type& vt, void* p, size_t bytes, 
 // Pinned staging for host-to-device uploads: the Tier-2 paths upload locals
 // that go out of scope before the stream drains, so every upload is first
 // copied into a pinned slot (then a true async DMA); a slot is reused only
-// after the event recorded behind its copy.
+// after the event recorded behind its copy.  Uploads above kMaxSlotBytes
+// (e.g. DCF BatchEvaluate's per-key correction words at 2^20 keys, ~0.5 GiB)
+// do not grow a slot: they are copied straight from the caller's memory and
+// the stream is drained before returning, so no thread keeps GBs of pinned
+// memory for the life of the process.
 class UploadRing {
  public:
   UploadRing() = default;
@@ -263,6 +284,15 @@ class UploadRing {
   Status CopyPacked(void* dst, const HostPart* parts, int k, size_t bytes, const size_t* off,
                     hipStream_t s) {
     if (bytes == 0) return OkStatus();
+    if (bytes > kMaxSlotBytes) {
+      for (int i = 0; i < k; ++i)
+        if (parts[i].bytes)
+          DPF_RETURN_IF_ERROR(HipStatus(
+              hipMemcpyAsync(static_cast<char*>(dst) + (off ? off[i] : 0), parts[i].p,
+                             parts[i].bytes, hipMemcpyHostToDevice, s),
+              "upload"));
+      return HipStatus(hipStreamSynchronize(s), "upload sync");
+    }
     Slot& sl = slots_[next_];
     next_ = (next_ + 1) % kSlots;
     if (sl.done == nullptr)
@@ -314,6 +344,7 @@ class UploadRing {
     return m;
   }
   static constexpr int kSlots = 16;
+  static constexpr size_t kMaxSlotBytes = size_t{16} << 20;
   struct Slot {
     void* host = nullptr;
     void* dev = nullptr;  // device address of `host`
@@ -334,12 +365,17 @@ inline UploadRing& ThreadUploadRing() {
 // handed EvaluateUntil memory that kernels saw with wrong contents (c3 at
 // 2^16 prefixes: gather offsets out of range, or a wrong share at alpha at
 // hierarchy level 5 — also with kernels and copies serialized), while the
-// same binary on ROCm 7.0's runtime and on plain hipMalloc was bit-exact.
+// same binary on ROCm 7.0's runtime and on plain hipMalloc was bit-exact
+// (tools/malloc_async_repro.cc reproduces the pattern outside the library).
 // A freed block keeps an event recorded on the freeing stream; it is handed
 // out again at once on that stream (stream order covers the reuse) and on
-// any other stream once the event has completed.  Blocks stay cached (sizes
-// rounded to powers of two up to 1 MiB, 2 MiB multiples above) until an
-// allocation fails, which releases the idle ones and retries.
+// any other stream once the event has completed.  Sizes are rounded to
+// powers of two up to 1 MiB and to 2 MiB multiples above; a request may take
+// an idle block up to 25 % larger than its bucket.  Idle blocks are bounded:
+// above DPF_AMD_POOL_CACHE_MB (default 4096) of idle memory the least
+// recently freed blocks go back to the device, and an allocation that fails
+// (here or in a caller, through dpf_amd_release_cached_memory) releases all
+// idle blocks and retries.
 class DevicePool {
  public:
   static DevicePool& Get() {
@@ -353,8 +389,9 @@ class DevicePool {
     DPF_RETURN_IF_ERROR(HipStatus(hipGetDevice(&dev), "hipGetDevice"));
     {
       std::lock_guard<std::mutex> l(mu_);
-      auto range = free_.equal_range(std::make_pair(dev, size));
-      for (auto it = range.first; it != range.second; ++it) {
+      const size_t limit = size + size / 4;
+      for (auto it = free_.lower_bound(std::make_pair(dev, size));
+           it != free_.end() && it->first.first == dev && it->first.second <= limit; ++it) {
         Block& b = it->second;
         if (b.stream != s && hipEventQuery(b.ready) != hipSuccess) {
           // not-ready is the expected answer; clear it so the next launch
@@ -364,8 +401,8 @@ class DevicePool {
         }
         *out = b.p;
         events_.push_back(b.ready);
-        live_[b.p] = std::make_pair(size, dev);
-        cached_ -= size;
+        live_[b.p] = std::make_pair(b.size, dev);
+        cached_ -= b.size;
         free_.erase(it);
         return OkStatus();
       }
@@ -389,7 +426,7 @@ class DevicePool {
     std::lock_guard<std::mutex> l(mu_);
     auto it = live_.find(p);
     if (it == live_.end()) return;
-    Block b{p, it->second.first, s, nullptr};
+    Block b{p, it->second.first, s, nullptr, ++seq_};
     const int dev = it->second.second;
     live_.erase(it);
     if (!events_.empty()) {
@@ -406,19 +443,18 @@ class DevicePool {
     }
     free_.emplace(std::make_pair(dev, b.size), b);
     cached_ += b.size;
+    if (cached_ > CacheLimit()) TrimLocked(CacheLimit());
   }
 
-  // Returns idle cached blocks to the device (allocation failure path).
+  // Returns every idle cached block to the device.
   void Release() {
     std::lock_guard<std::mutex> l(mu_);
-    for (auto it = free_.begin(); it != free_.end();) {
-      Block& b = it->second;
-      if (b.ready) (void)hipEventSynchronize(b.ready);
-      (void)hipFree(b.p);
-      if (b.ready) events_.push_back(b.ready);
-      cached_ -= b.size;
-      it = free_.erase(it);
-    }
+    TrimLocked(0);
+  }
+
+  size_t cached_bytes() {
+    std::lock_guard<std::mutex> l(mu_);
+    return cached_;
   }
 
  private:
@@ -427,7 +463,34 @@ class DevicePool {
     size_t size;
     hipStream_t stream;
     hipEvent_t ready;
+    uint64_t seq;  // free order (least recently freed is trimmed first)
   };
+  static size_t CacheLimit() {
+    static const size_t lim = [] {
+      const char* e = std::getenv("DPF_AMD_POOL_CACHE_MB");
+      return (e ? std::strtoull(e, nullptr, 10) : 4096ull) << 20;
+    }();
+    return lim;
+  }
+  // Frees idle blocks, least recently freed first, until at most `keep`
+  // bytes stay cached (caller holds mu_).
+  void TrimLocked(size_t keep) {
+    if (cached_ <= keep) return;
+    std::vector<std::multimap<std::pair<int, size_t>, Block>::iterator> order;
+    order.reserve(free_.size());
+    for (auto it = free_.begin(); it != free_.end(); ++it) order.push_back(it);
+    std::sort(order.begin(), order.end(),
+              [](const auto& x, const auto& y) { return x->second.seq < y->second.seq; });
+    for (auto it : order) {
+      if (cached_ <= keep) break;
+      Block& b = it->second;
+      if (b.ready) (void)hipEventSynchronize(b.ready);
+      (void)hipFree(b.p);
+      if (b.ready) events_.push_back(b.ready);
+      cached_ -= b.size;
+      free_.erase(it);
+    }
+  }
   static size_t Bucket(size_t n) {
     if (n <= (size_t{1} << 20)) {
       size_t b = 512;
@@ -442,6 +505,7 @@ class DevicePool {
   std::multimap<std::pair<int, size_t>, Block> free_;        // (device, size) -> idle block
   std::vector<hipEvent_t> events_;                           // recycled
   size_t cached_ = 0;
+  uint64_t seq_ = 0;
 };
 
 // DPF_AMD_DEBUG_ALLOC=1: every live DeviceBuffer range is registered and a

@@ -397,14 +397,14 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
                             x[2] ^ x[3], x[0] ^ x[2] ^ x[3], x[1] ^ x[2] ^ x[3], x012 ^ x[3]};
 #if DPF_SCAN_M4_ADDTID
     // ds_write_addtid_b32 (address = M0 + offset + 4 * lane): no address
-    // VGPRs and half the LDS transfer cycles of ds_write_b32.  M0 is set in
-    // the same asm statement, so no compiler-held M0 value is assumed after;
-    // the compiler's hazard recognizer does not see inside the asm, so the
-    // wait state an add-TID op needs after an SALU write of M0 is explicit
-    // (without it, rows were written elsewhere at random: nondeterministic
-    // 2^26-record scans, tools/diag_scan_determinism.py).
+    // VGPRs and half the LDS transfer cycles of ds_write_b32.  The table
+    // base is bound to M0 as an "{m0}" input operand, so the compiler writes
+    // M0 itself and knows its value at every point.  Its hazard recognizer
+    // does not see inside the asm, so the wait state an add-TID op needs
+    // after an SALU write of M0 is explicit (without it, rows were written
+    // elsewhere at random: nondeterministic 2^26-record scans,
+    // tools/diag_scan_determinism.py).
     asm volatile(
-        "s_mov_b32 m0, %15\n\t"
         "s_nop 0\n\t"  // SALU write of M0 -> LDS add-TID op: 1 wait state
         "ds_write_addtid_b32 %0 offset:272\n\tds_write_addtid_b32 %1 offset:544\n\t"
         "ds_write_addtid_b32 %2 offset:816\n\tds_write_addtid_b32 %3 offset:1088\n\t"
@@ -417,7 +417,7 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
         :
         : "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]),
           "v"(r[8]), "v"(r[9]), "v"(r[10]), "v"(r[11]), "v"(r[12]), "v"(r[13]), "v"(r[14]),
-          "v"(r[15]), "s"((uint32_t)(uintptr_t)t)
+          "v"(r[15]), "{m0}"((uint32_t)(uintptr_t)t)
         : "memory");
     static_assert(ROW * 16 == 272, "addtid offsets assume 272-byte rows");
 #else

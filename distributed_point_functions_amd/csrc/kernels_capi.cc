@@ -19,11 +19,15 @@ namespace dpf_amd {
 
 namespace {
 
-std::atomic<int> g_expand_depth{0};  // dpf_amd_set_expand_depth (tests)
-std::atomic<int> g_scan_m4{[] {      // dpf_amd_set_scan_m4 (tests, A/B)
+// Test hooks, per calling thread: a test forcing a kernel variant never
+// changes what another thread's launches pick.
+thread_local int t_expand_depth = 0;  // dpf_amd_set_expand_depth
+// dpf_amd_set_scan_m4; the process default comes from DPF_AMD_SCAN_M4 (A/B runs)
+const int kScanM4Default = [] {
   const char* e = std::getenv("DPF_AMD_SCAN_M4");
   return e ? std::atoi(e) : -1;
-}()};
+}();
+thread_local int t_scan_m4 = kScanM4Default;
 
 int GridFor(int64_t items, int block, int max_blocks) {
   int64_t g = (items + block - 1) / block;
@@ -248,7 +252,7 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
   const int64_t range = leaf_end - leaf_begin;
   if (D == 8 && (range >> 8) < (int64_t{1} << 17)) D = 4;
   if (D == 4 && (range >> 4) < (int64_t{1} << 16)) D = 2;
-  const int forced = g_expand_depth.load(std::memory_order_relaxed);
+  const int forced = t_expand_depth;
   if (forced > 0 && forced <= num_levels) D = forced;
   ExpandArgs a;
   a.root_seeds = (const uint4*)root_seeds;
@@ -270,12 +274,16 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
 
 int dpf_amd_set_expand_depth(int depth) {
   if (depth != 0 && depth != 1 && depth != 2 && depth != 4 && depth != 8) return -1;
-  return g_expand_depth.exchange(depth);
+  const int old = t_expand_depth;
+  t_expand_depth = depth;
+  return old;
 }
 
 int dpf_amd_set_scan_m4(int mode) {
   if (mode < -1 || mode > 1) return -2;
-  return g_scan_m4.exchange(mode);
+  const int old = t_scan_m4;
+  t_scan_m4 = mode;
+  return old;
 }
 
 // Shared body of dpf_amd_evaluate_points{,_batched}.
@@ -440,7 +448,7 @@ static int ScanGrid(int64_t num_records, int num_queries, int64_t record_stride)
 // Mode (dpf_amd_set_scan_m4 / DPF_AMD_SCAN_M4): 0 never, 1 always (tests),
 // -1 from kScanM4MinQueries queries on.
 static bool UseScanM4(int rem, int C) {
-  const int mode = g_scan_m4.load();
+  const int mode = t_scan_m4;
   if (mode == 0) return false;
   if (C > (1 << 16)) return false;  // records > 1 MiB: 128-record tiles past 2^27 B
   if (mode < 0 && (rem < kScanM4MinQueries || C < 4)) return false;

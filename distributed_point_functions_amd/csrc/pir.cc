@@ -98,7 +98,14 @@ StatusOr<std::unique_ptr<DenseDpfPirDatabase::Interface>> DenseDpfPirDatabase::B
   // width onto the wave, so no padding is read or stored).
   db->stride_ = std::max<int64_t>(16, AlignBytes(max_size));
   const int64_t bytes = std::max<int64_t>(16, n * db->stride_);
-  DPF_RETURN_IF_ERROR(HipStatus(hipMalloc(&db->records_, bytes), "hipMalloc(database)"));
+  hipError_t e = hipMalloc(&db->records_, bytes);
+  if (e == hipErrorOutOfMemory) {
+    // idle blocks cached by earlier Tier-2 calls go back to the device first
+    (void)hipGetLastError();
+    dpf_internal_host::DevicePool::Get().Release();
+    e = hipMalloc(&db->records_, bytes);
+  }
+  DPF_RETURN_IF_ERROR(HipStatus(e, "hipMalloc(database)"));
   DPF_RETURN_IF_ERROR(HipStatus(hipMemset(db->records_, 0, bytes), "hipMemset(database)"));
   // Upload in 64 MiB chunks of zero-padded fixed-stride rows.
   const int64_t rows_per_chunk = std::max<int64_t>(1, (64 << 20) / db->stride_);

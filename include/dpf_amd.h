@@ -81,6 +81,11 @@ const char* dpf_amd_last_error(void);
 /* Library / device info. */
 int dpf_amd_device_count(int* count);
 const char* dpf_amd_version(void);
+/* Returns the idle device blocks the library's caching allocator holds to
+ * the device (a caller about to make a large allocation of its own, e.g. a
+ * database or a torch tensor, after Tier-2 calls left blocks cached); writes
+ * the bytes released to *released (may be NULL). */
+int dpf_amd_release_cached_memory(int64_t* released);
 
 /* ------------------------------------------------------------------------ */
 /* Tier 1: device seams                                                     */
@@ -131,17 +136,19 @@ int dpf_amd_expand_and_correct(
     int corrected_elements_per_block, int64_t leaf_begin, int64_t leaf_end,
     void* out, void* stream);
 
-/* Testing knob (process-wide): forces the register-DFS depth D of the fused
+/* Testing knob (calling thread only): forces the register-DFS depth D of the fused
  * expansion kernel to 1, 2, 4 or 8 whenever num_levels >= D, so the deep
  * kernels that large launches select can be checked on small domains.
  * 0 restores the automatic choice.  Returns the previous setting, or -1 for
  * an invalid depth (setting unchanged). */
 int dpf_amd_set_expand_depth(int depth);
 
-/* Testing knob (process-wide): which XOR scan dpf_amd_inner_product runs.
+/* Testing knob (calling thread only): which XOR scan dpf_amd_inner_product
+ * runs on launches issued by this thread.
  * -1 automatic (the Four-Russians many-query scan from 16 queries on, records
  * of >= 64 bytes; the masked scan otherwise), 0 always the masked scan, 1
- * always the Four-Russians scan.  The default comes from DPF_AMD_SCAN_M4.
+ * always the Four-Russians scan.  Every thread starts from DPF_AMD_SCAN_M4
+ * (or -1).
  * Returns the previous setting, or -2 for an invalid mode (unchanged). */
 int dpf_amd_set_scan_m4(int mode);
 

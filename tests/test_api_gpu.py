@@ -383,3 +383,48 @@ def test_incremental_unsorted_duplicate_and_missing_prefixes(api):
         od.evaluate_until(2, [(7 << 8) | 1], octx)
     assert "Prefix not present in ctx.partial_evaluations" in str(ours.value)
     assert str(ours.value).split(":")[-1].strip() == str(ref.value).split(":")[-1].strip()
+
+
+def test_incremental_duplicate_partial_evaluation_past_the_queries(api):
+    """A duplicate stored prefix with a mismatching seed is rejected wherever
+    it sits in ctx.partial_evaluations (cc:390-405 builds its btree from the
+    whole list), including after the last entry a sorted query reaches; a
+    duplicate with the same seed and control bit is accepted."""
+    from distributed_point_functions_amd import wire
+    D, V, _ = api
+    spec = ("int", 64)
+    levels = [(ld, spec, 40 + ld) for ld in (8, 16, 24)]
+    rng = random.Random(78)
+    alpha = rng.getrandbits(24)
+    betas = [rng.getrandbits(64) for _ in levels]
+    seeds = (rng.getrandbits(128), rng.getrandbits(128))
+    dpf = _make(api, levels)
+    od = po.Dpf(levels)
+    k0, _ = dpf.generate_keys_incremental(alpha, betas, seeds=seeds)
+    ok0, _ = od.generate_keys(alpha, betas, seeds=seeds)
+    vt = V.from_spec(spec)
+    ctx = dpf.create_evaluation_context(k0)
+    octx = od.create_evaluation_context(ok0)
+    dpf.evaluate_next([], ctx, raw=True)
+    od.evaluate_until(0, [], octx)
+    p1 = list(range(40))
+    assert vt.decode_flat(dpf.evaluate_next(p1, ctx, raw=True)) == od.evaluate_until(1, p1, octx)
+    pes = ctx.partial_evaluations()
+    assert len(pes) > 2 and [p for p, _, _ in pes] == sorted({p for p, _, _ in pes})
+    last_prefix, last_seed, last_cb = pes[-1]
+    p2 = [(0 << 8) | 3, (1 << 8) | 9]  # their stored parents come first in the list
+
+    def with_extra(seed, cb):
+        pe = (wire.field_bytes(1, wire.block(last_prefix)) +
+              wire.field_bytes(2, wire.block(seed)) + wire.field_varint(3, int(cb)))
+        return dpf.parse_evaluation_context(ctx.serialize() + wire.field_bytes(4, pe))
+
+    with pytest.raises(Exception) as e:
+        dpf.evaluate_next(p2, with_extra(last_seed ^ (1 << 77), last_cb), raw=True)
+    assert "Duplicate prefix in `ctx.partial_evaluations()` with mismatching seed or " \
+           "control bit" in str(e.value)
+    with pytest.raises(Exception) as e:
+        dpf.evaluate_next(p2, with_extra(last_seed, not last_cb), raw=True)
+    assert "Duplicate prefix" in str(e.value)
+    same = with_extra(last_seed, last_cb)
+    assert vt.decode_flat(dpf.evaluate_next(p2, same, raw=True)) == od.evaluate_until(2, p2, octx)

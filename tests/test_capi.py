@@ -50,3 +50,27 @@ def test_no_torch_types_in_the_abi():
     text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)  # code, not comments
     for bad in ("torch", "at::", "c10", "std::", "Tensor"):
         assert bad not in text
+
+
+def test_kernel_choice_hooks_are_per_thread():
+    """dpf_amd_set_expand_depth / dpf_amd_set_scan_m4 change only the calling
+    thread's launches (no GPU needed: the setters touch no device state)."""
+    import threading
+    from distributed_point_functions_amd import _lib
+    L = _lib.lib()
+    assert L.dpf_amd_set_expand_depth(4) == 0
+    assert L.dpf_amd_set_scan_m4(1) in (-1, 0, 1)
+    seen = {}
+
+    def other():
+        seen["depth"] = L.dpf_amd_set_expand_depth(2)
+        seen["depth_back"] = L.dpf_amd_set_expand_depth(0)
+        seen["scan"] = L.dpf_amd_set_scan_m4(0)
+
+    t = threading.Thread(target=other)
+    t.start()
+    t.join()
+    assert seen["depth"] == 0 and seen["depth_back"] == 2
+    assert seen["scan"] != 1 or os.environ.get("DPF_AMD_SCAN_M4") == "1"
+    assert L.dpf_amd_set_expand_depth(0) == 4
+    assert L.dpf_amd_set_scan_m4(-1) == 1

@@ -170,7 +170,12 @@ def c5_full(K, cuda):
 
 def test_c5_full_domain_share_sum_on_device(c5_full):
     """out0 + out1 == beta at alpha and 0 at every other of the 2^32 leaves
-    (u32 wraps mod 2^32, IntModN adds mod p = 2^64 - 59)."""
+    (u32 wraps mod 2^32, IntModN adds mod p = 2^64 - 59).
+
+    This is an alpha-path check: off the path both parties hold the same seed
+    and control bit (cc:196-209), so any deterministic function of the seed
+    sums to 0 there after party 1's negation.  The bit-exact pin of every
+    leaf is test_c5_full_domain_every_subtree_digest_matches_oracle."""
     import torch
     n, alpha = c5_full["n"], c5_full["alpha"]
     a = c5_full["outs"][0].view(torch.int64).view(-1, 2)
@@ -194,6 +199,72 @@ def test_c5_full_domain_share_sum_on_device(c5_full):
     beta0, beta1 = c5_full["beta"]
     assert (xa[1] + xb[1]) % (1 << 32) == beta0
     assert (xa[0] + xb[0]) % P64 == beta1
+
+
+def _device_subtree_sha256(out, log_sub=20, subs_per_chunk=64, workers=16):
+    """SHA-256 of every 2^log_sub-leaf (16 B/leaf) slice of a device buffer:
+    1 GiB chunks copied into two pinned host buffers on a side stream (the
+    copy of chunk c + 1 overlaps the hashing of chunk c), each chunk's
+    16 MiB slices hashed by a thread pool (hashlib releases the GIL)."""
+    import concurrent.futures as cf
+    import hashlib
+    import torch
+    sub = 16 << log_sub
+    chunk = sub * subs_per_chunk
+    total = out.numel()
+    assert total % chunk == 0
+    nchunks = total // chunk
+    bufs = [torch.empty(chunk, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    views = [memoryview(b.numpy()) for b in bufs]
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    done = [torch.cuda.Event(), torch.cuda.Event()]
+
+    def issue(c):
+        with torch.cuda.stream(side):
+            bufs[c % 2].copy_(out[c * chunk:(c + 1) * chunk], non_blocking=True)
+            done[c % 2].record(side)
+
+    digests = []
+    with cf.ThreadPoolExecutor(workers) as ex:
+        issue(0)
+        for c in range(nchunks):
+            done[c % 2].synchronize()
+            if c + 1 < nchunks:
+                issue(c + 1)  # the other buffer: its hashes finished last iteration
+            v = views[c % 2]
+            digests += list(ex.map(lambda i: hashlib.sha256(v[i * sub:(i + 1) * sub]).hexdigest(),
+                                   range(subs_per_chunk)))
+    return digests
+
+
+def test_c5_full_domain_every_subtree_digest_matches_oracle(c5_full):
+    """Bit-exact parity of all 2 x 2^32 leaf values of the headline launch:
+    the SHA-256 of each 2^20-leaf subtree of both parties' device output
+    (host layout) equals the oracle's (tests/golden/c5_subtree_digests.json,
+    written by tests/golden/make_c5_digests.py from oracle/dpf_oracle.c for
+    this same key: ExpandSeeds cc:289-372, HashExpandedSeeds cc:523-547, the
+    correction loop h:846-862)."""
+    import json
+    import os
+    import time
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                        "c5_subtree_digests.json")
+    with open(path) as f:
+        gold = json.load(f)
+    d, k0, k1, alpha, beta = _keys(C5, 32, seed=5)
+    assert (gold["alpha"], tuple(gold["beta"])) == (alpha, tuple(beta))
+    assert gold["log_subtree_leaves"] == 20
+    for party in (0, 1):
+        t0 = time.time()
+        got = _device_subtree_sha256(c5_full["outs"][party])
+        want = gold["sha256"][str(party)]
+        assert len(got) == len(want) == 4096
+        bad = [i for i in range(4096) if got[i] != want[i]]
+        print("party %d: 4096 subtree digests in %.1f s, %d differ" %
+              (party, time.time() - t0, len(bad)))
+        assert not bad, "party %d: %d of 4096 subtrees differ from the oracle (first %s)" % (
+            party, len(bad), bad[:8])
 
 
 def test_c5_full_domain_sampled_subtrees_match_oracle(c5_full):

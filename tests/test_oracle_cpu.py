@@ -258,3 +258,34 @@ def test_aes_ctr_prng_matches_libcrypto(seed_hex, length):
     assert po.aes_ctr_prng(seed, length) == want
     # GetRandomBytes in pieces continues the same stream (test.cc:81-91)
     assert _evp_aes_128_ctr(seed, bytes(16), [7, 0, 16, 1, length - 24]) == want
+
+
+def test_c5_subtree_digest_fixture_matches_oracle():
+    """The committed per-subtree digests of the headline key
+    (tests/golden/c5_subtree_digests.json, 2 x 4096 SHA-256) are the
+    oracle's: recompute the first, alpha's and the last subtree of both
+    parties (the GPU test compares all 8192 with the device output)."""
+    import hashlib
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_c5_digests as mk
+    with open(mk.OUT) as f:
+        gold = json.load(f)
+    alpha, beta, seeds = mk.key_params()
+    assert gold["alpha"] == alpha and tuple(gold["beta"]) == beta
+    assert [int(s) for s in gold["keygen_seeds"]] == list(seeds)
+    d = po.Dpf([(mk.LOG_DOMAIN, mk.SPEC, mk.SECURITY)])
+    keys = d.generate_keys(alpha, [beta], seeds=seeds)
+    nsub = 1 << (mk.LOG_DOMAIN - mk.LOG_SUBTREE)
+    for party in (0, 1):
+        assert len(gold["sha256"][str(party)]) == nsub
+        for s in (0, alpha >> mk.LOG_SUBTREE, nsub - 1):
+            words = d.expand_subtree_words(keys[party], s << mk.LOG_SUBTREE,
+                                           mk.LOG_SUBTREE).reshape(-1, 2, 2)
+            got = hashlib.sha256(mk.host_layout_bytes(words)).hexdigest()
+            assert got == gold["sha256"][str(party)][s], (party, s)
+    # party 1 holds the negated shares, so no subtree digest of the two
+    # parties coincides (the fixture is not degenerate)
+    assert not set(gold["sha256"]["0"]) & set(gold["sha256"]["1"])
+    assert len(set(gold["sha256"]["0"])) == nsub
