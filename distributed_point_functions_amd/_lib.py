@@ -141,6 +141,7 @@ def _bind_tier2(L):
     _sig(L, "dpf_amd_evaluate_until_device", I32, P, I32, P, I64, P, SZ, P, P, I64,
          ctypes.POINTER(I64), P)
     _sig(L, "dpf_amd_evaluate_at", I32, P, P, SZ, I32, P, I64, P, SZ, P)
+    _sig(L, "dpf_amd_expand_leaves_on_devices", I32, P, P, SZ, I32, P, P, P, P)
     _sig(L, "dpf_amd_evaluate_and_apply", I32, P, P, P, I64, P, I32, P, SZ, P, APPLY_FN, P)
     _sig(L, "dpf_amd_dcf_create", I32, P, SZ, PP)
     _sig(L, "dpf_amd_dcf_destroy", None, P)
@@ -156,6 +157,10 @@ def _bind_tier2(L):
     _sig(L, "dpf_amd_pir_db_max_value_size", I64, P)
     _sig(L, "dpf_amd_pir_db_device_records", P, P, ctypes.POINTER(I64))
     _sig(L, "dpf_amd_pir_db_inner_product", I32, P, P, I64, I32, P)
+    _sig(L, "dpf_amd_pir_db_set_devices", I32, P, P, I32)
+    _sig(L, "dpf_amd_pir_db_num_shards", I32, P)
+    _sig(L, "dpf_amd_pir_db_shard", I32, P, I32, ctypes.POINTER(ctypes.c_int),
+         ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.POINTER(P))
     _sig(L, "dpf_amd_pir_server_create_plain", I32, P, SZ, P, PP)
     _sig(L, "dpf_amd_pir_server_destroy", None, P)
     _sig(L, "dpf_amd_pir_call_while_waiting", I32, P)

@@ -1,5 +1,6 @@
 // capi.cc — Tier-2 C ABI (include/dpf_amd.h): the reference's public objects
 // behind opaque handles, with protos exchanged in wire format.
+#include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -236,6 +237,22 @@ int dpf_amd_evaluate_until_device(const dpf_amd_dpf* dpf, int hierarchy_level,
                            stream);
 }
 
+int dpf_amd_expand_leaves_on_devices(const dpf_amd_dpf* dpf, const uint8_t* key, size_t key_len,
+                                     int num_slices, const int* devices,
+                                     const int64_t* leaf_begin, const int64_t* leaf_end,
+                                     void* const* outs) {
+  DpfKey k;
+  if (!k.ParseFromArray(key, key_len)) return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed DpfKey proto");
+  if (num_slices < 0) return Fail(DPF_AMD_INVALID_ARGUMENT, "negative number of slices");
+  const size_t n = static_cast<size_t>(num_slices);
+  const int h = dpf->dpf->num_hierarchy_levels() - 1;
+  Status st = dpf->dpf->ExpandLeavesOnDevices(
+      k, Span<const int>(devices, n), Span<const int64_t>(leaf_begin, n),
+      Span<const int64_t>(leaf_end, n), Span<void* const>(outs, n),
+      dpf->dpf->value_type_descriptor(h));
+  return st.ok() ? DPF_AMD_OK : Fail(st);
+}
+
 int dpf_amd_evaluate_at(const dpf_amd_dpf* dpf, const uint8_t* key, size_t key_len,
                         int hierarchy_level, const uint64_t* points, int64_t num_points,
                         const uint8_t* value_type, size_t value_type_len, void* out) {
@@ -389,6 +406,38 @@ int dpf_amd_release_cached_memory(int64_t* released) {
   const size_t before = pool.cached_bytes();
   pool.Release();
   if (released) *released = static_cast<int64_t>(before - pool.cached_bytes());
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_pir_db_set_devices(dpf_amd_pir_db* db, const int* devices, int num_devices) {
+  if (!db->builder) return Fail(DPF_AMD_FAILED_PRECONDITION, "Database already built");
+  if (num_devices < 0 || (num_devices > 0 && devices == nullptr))
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "bad device list");
+  int count = 0;
+  if (num_devices > 0 && hipGetDeviceCount(&count) != hipSuccess)
+    return Fail(DPF_AMD_INTERNAL, "hipGetDeviceCount failed");
+  for (int i = 0; i < num_devices; ++i)
+    if (devices[i] < 0 || devices[i] >= count)
+      return Fail(DPF_AMD_INVALID_ARGUMENT, "device " + std::to_string(devices[i]) +
+                                                " out of range [0, " + std::to_string(count) + ")");
+  db->builder->SetDevices(std::vector<int>(devices, devices + num_devices));
+  return DPF_AMD_OK;
+}
+
+int dpf_amd_pir_db_num_shards(const dpf_amd_pir_db* db) {
+  return db->gpu() ? static_cast<int>(db->gpu()->shards().size()) : 0;
+}
+
+int dpf_amd_pir_db_shard(const dpf_amd_pir_db* db, int shard, int* device, int64_t* row_begin,
+                         int64_t* row_end, const void** records) {
+  if (!db->gpu()) return Fail(DPF_AMD_FAILED_PRECONDITION, "database not built");
+  const auto& sh = db->gpu()->shards();
+  if (shard < 0 || shard >= static_cast<int>(sh.size()))
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "shard out of range");
+  if (device) *device = sh[shard].device;
+  if (row_begin) *row_begin = sh[shard].row_begin;
+  if (row_end) *row_end = sh[shard].row_end;
+  if (records) *records = sh[shard].records;
   return DPF_AMD_OK;
 }
 

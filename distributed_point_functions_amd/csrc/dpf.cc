@@ -724,6 +724,7 @@ using dpf_internal_host::DeviceBuffer;
 using dpf_internal_host::HipStatus;
 using dpf_internal_host::HostTrace;
 using dpf_internal_host::ThreadStream;
+using dpf_internal_host::StreamSyncGuard;
 using dpf_internal_host::ThreadUploadRing;
 using dpf_internal_host::UploadRing;
 
@@ -1189,9 +1190,11 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
   trace.Mark("upload+walk_launch");
   ctx.clear_partial_evaluations();
   if (update_ctx && n > 0) {
+    StreamSyncGuard drain(s);  // no copy left in flight into seeds / cbs on an error
     DPF_RETURN_IF_ERROR(CopyToHost(seeds.get(), *seeds_dev, 16 * n, s));
     DPF_RETURN_IF_ERROR(CopyToHost(cbs.get(), *cb_dev, n, s));
     DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+    drain.Dismiss();
     std::vector<PartialEvaluation>* pe = ctx.mutable_partial_evaluations();
     pe->resize(n);
     for (int64_t i = 0; i < n; ++i) {
@@ -1327,6 +1330,8 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
 
   DeviceBuffer staging, result, gather_err, src_dev;
   int gather_flag = 0;
+  // an error return must not leave the async D2H of gather_flag in flight
+  StreamSyncGuard drain(s);
   void* gather_src_dev = nullptr;
   std::vector<int64_t> gather_src_host;
   void* expand_out = nullptr;
@@ -1395,6 +1400,7 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
     }
     return InternalError("gather offsets corrupted between host and device" + detail);
   }
+  drain.Dismiss();  // the stream was drained above
   trace.Mark("gather+copy+sync");
   ctx.set_previous_hierarchy_level(hierarchy_level);
   return OkStatus();
@@ -1615,18 +1621,58 @@ Status DistributedPointFunction::ExpandLeavesOnDevice(const DpfKey& key, int64_t
 }
 
 
+Status DistributedPointFunction::ExpandLeavesOnDevices(const DpfKey& key, Span<const int> devices,
+                                                       Span<const int64_t> leaf_begin,
+                                                       Span<const int64_t> leaf_end,
+                                                       Span<void* const> outs,
+                                                       const dpf_amd_value_type& layout) const {
+  const size_t n = devices.size();
+  if (leaf_begin.size() != n || leaf_end.size() != n || outs.size() != n)
+    return InvalidArgumentError("`devices`, `leaf_begin`, `leaf_end` and `outs` must have the "
+                                "same size");
+  DPF_RETURN_IF_ERROR(ValidateDpfKey(*state_, key));
+  // Issue every device's launch first (each on this thread's stream for that
+  // device), then wait for all of them.
+  Status st = OkStatus();
+  std::vector<hipStream_t> streams(n, nullptr);
+  for (size_t i = 0; i < n && st.ok(); ++i) {
+    dpf_internal_host::DeviceGuard g(devices[i]);
+    streams[i] = dpf_internal_host::ThreadStreamOn(devices[i]);
+    if (streams[i] == nullptr) {
+      st = InternalError("no stream on device " + std::to_string(devices[i]));
+      break;
+    }
+    st = ExpandLeavesOnDevice(key, leaf_begin[i], leaf_end[i], layout, outs[i], streams[i]);
+  }
+  for (size_t i = 0; i < n; ++i) {
+    if (streams[i] == nullptr) continue;
+    dpf_internal_host::DeviceGuard g(devices[i]);
+    Status w = HipStatus(hipStreamSynchronize(streams[i]), "sync");
+    if (st.ok()) st = w;
+  }
+  return st;
+}
+
 Status DistributedPointFunction::ExpandLeavesOnDeviceBatched(Span<const DpfKey* const> keys,
                                                              int64_t num_leaves,
                                                              const dpf_amd_value_type& layout,
                                                              void* out, void* stream) const {
+  return ExpandLeavesOnDeviceBatched(keys, 0, num_leaves, layout, out, stream);
+}
+
+Status DistributedPointFunction::ExpandLeavesOnDeviceBatched(Span<const DpfKey* const> keys,
+                                                             int64_t leaf_begin, int64_t leaf_end,
+                                                             const dpf_amd_value_type& layout,
+                                                             void* out, void* stream) const {
   const DpfState& st = *state_;
   const int64_t q = static_cast<int64_t>(keys.size());
+  const int64_t num_leaves = leaf_end - leaf_begin;
   if (q == 0 || num_leaves <= 0) return OkStatus();
   for (const DpfKey* k : keys) DPF_RETURN_IF_ERROR(ValidateDpfKey(st, *k));
   const int h = num_hierarchy_levels() - 1;
   const LevelMeta& m = st.levels[h];
   if (m.tree_level > 62) return InvalidArgumentError("domain too large to expand fully");
-  if (num_leaves > (int64_t{1} << m.tree_level))
+  if (leaf_begin < 0 || leaf_end > (int64_t{1} << m.tree_level))
     return InvalidArgumentError("leaf range out of bounds");
   dpf_amd_value_type vt;
   DPF_RETURN_IF_ERROR(MergeLayout(m, layout, &vt));
@@ -1640,7 +1686,7 @@ Status DistributedPointFunction::ExpandLeavesOnDeviceBatched(Span<const DpfKey* 
   char* o = static_cast<char*>(out);
   if (!walk) {
     for (int64_t i = 0; i < q; ++i)
-      DPF_RETURN_IF_ERROR(ExpandLeavesOnDevice(*keys[i], 0, num_leaves, layout,
+      DPF_RETURN_IF_ERROR(ExpandLeavesOnDevice(*keys[i], leaf_begin, leaf_end, layout,
                                                o + i * num_leaves * cepb * vt.out_stride, stream));
     return OkStatus();
   }
@@ -1674,11 +1720,10 @@ Status DistributedPointFunction::ExpandLeavesOnDeviceBatched(Span<const DpfKey* 
   DeviceBuffer dev;
   DPF_RETURN_IF_ERROR(dev.Upload(host.data(), host.size(), s));
   char* d = dev.as<char>();
-  return AbiStatus(dpf_amd_evaluate_points_batched(
-      q, num_leaves, d, reinterpret_cast<const uint8_t*>(d + off_cb), nullptr, 0, L, d + off_cw,
+  return AbiStatus(dpf_amd::EvaluatePointsBatchedRange(
+      q, leaf_begin, num_leaves, d, reinterpret_cast<const uint8_t*>(d + off_cb), L, d + off_cw,
       reinterpret_cast<const uint8_t*>(d + off_ccl), reinterpret_cast<const uint8_t*>(d + off_ccr),
-      &vt, nullptr, reinterpret_cast<const int8_t*>(d + off_party), 0, d + off_corr, nullptr, out,
-      s));
+      &vt, reinterpret_cast<const int8_t*>(d + off_party), d + off_corr, out, s));
 }
 
 }  // namespace distributed_point_functions

@@ -55,6 +55,47 @@ inline hipStream_t ThreadStream() {
   return h.s;
 }
 
+// Makes `device` current for the guard's scope (the HIP runtime's current
+// device is per thread) and restores the previous one.
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(int device) {
+    if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+    if (device >= 0 && device != prev_ && hipSetDevice(device) == hipSuccess) set_ = true;
+  }
+  ~DeviceGuard() {
+    if (set_ && prev_ >= 0) (void)hipSetDevice(prev_);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+
+ private:
+  int prev_ = -1;
+  bool set_ = false;
+};
+
+// The calling thread's stream on `device` (sharded databases and multi-GPU
+// expansions issue each device's work on its own stream from one thread).
+inline hipStream_t ThreadStreamOn(int device) {
+  struct Holder {
+    std::map<int, hipStream_t> s;
+    ~Holder() {
+      for (auto& kv : s) {
+        DeviceGuard g(kv.first);
+        (void)hipStreamDestroy(kv.second);
+      }
+    }
+  };
+  thread_local Holder h;
+  auto it = h.s.find(device);
+  if (it != h.s.end()) return it->second;
+  DeviceGuard g(device);
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  h.s[device] = st;
+  return st;
+}
+
 // Host-side phase timer: with DPF_AMD_TRACE_HOST set, Mark(name) prints the
 // wall time since the previous mark to stderr (the reference has no tracing;
 // this is how the Tier-2 host overhead is attributed).
@@ -295,6 +336,16 @@ class UploadRing {
     }
     Slot& sl = slots_[next_];
     next_ = (next_ + 1) % kSlots;
+    int dev = 0;
+    DPF_RETURN_IF_ERROR(HipStatus(hipGetDevice(&dev), "hipGetDevice"));
+    if (sl.done != nullptr && sl.device != dev) {
+      // the slot's event belongs to the device its last copy ran on; events
+      // are recorded on streams of their own device (s is on the current one)
+      DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(sl.done), "upload slot"));
+      (void)hipEventDestroy(sl.done);
+      sl.done = nullptr;
+    }
+    sl.device = dev;
     if (sl.done == nullptr)
       DPF_RETURN_IF_ERROR(HipStatus(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming),
                                     "hipEventCreate"));
@@ -350,6 +401,7 @@ class UploadRing {
     void* dev = nullptr;  // device address of `host`
     size_t cap = 0;
     hipEvent_t done = nullptr;
+    int device = -1;  // device of `done`
   };
   Slot slots_[kSlots];
   int next_ = 0;
@@ -400,7 +452,7 @@ class DevicePool {
           continue;
         }
         *out = b.p;
-        events_.push_back(b.ready);
+        events_[dev].push_back(b.ready);
         live_[b.p] = std::make_pair(b.size, dev);
         cached_ -= b.size;
         free_.erase(it);
@@ -429,9 +481,11 @@ class DevicePool {
     Block b{p, it->second.first, s, nullptr, ++seq_};
     const int dev = it->second.second;
     live_.erase(it);
-    if (!events_.empty()) {
-      b.ready = events_.back();
-      events_.pop_back();
+    DeviceGuard g(dev);  // events belong to the block's (and its stream's) device
+    std::vector<hipEvent_t>& evs = events_[dev];
+    if (!evs.empty()) {
+      b.ready = evs.back();
+      evs.pop_back();
     } else if (hipEventCreateWithFlags(&b.ready, hipEventDisableTiming) != hipSuccess) {
       b.ready = nullptr;
     }
@@ -484,9 +538,10 @@ class DevicePool {
     for (auto it : order) {
       if (cached_ <= keep) break;
       Block& b = it->second;
+      DeviceGuard g(it->first.first);
       if (b.ready) (void)hipEventSynchronize(b.ready);
       (void)hipFree(b.p);
-      if (b.ready) events_.push_back(b.ready);
+      if (b.ready) events_[it->first.first].push_back(b.ready);
       cached_ -= b.size;
       free_.erase(it);
     }
@@ -503,7 +558,7 @@ class DevicePool {
   std::mutex mu_;
   std::unordered_map<void*, std::pair<size_t, int>> live_;  // block -> (size, device)
   std::multimap<std::pair<int, size_t>, Block> free_;        // (device, size) -> idle block
-  std::vector<hipEvent_t> events_;                           // recycled
+  std::map<int, std::vector<hipEvent_t>> events_;            // recycled, per device
   size_t cached_ = 0;
   uint64_t seq_ = 0;
 };

@@ -54,4 +54,14 @@ int CopyFromMappedHost(void* dst, const void* mapped_src, size_t bytes, void* st
 int MakeVtDev(const dpf_amd_value_type& vt, const uint64_t* correction,
               int party, int cepb, VtDev* out);
 
+// dpf_amd_evaluate_points_batched with implicit paths over the tree-index
+// range [first_point, first_point + points_per_key) of every key (the leaf
+// range of a batched selection expansion on one shard of a database).
+int EvaluatePointsBatchedRange(int64_t num_keys, int64_t first_point, int64_t points_per_key,
+                               const void* key_seeds, const uint8_t* key_control_bits,
+                               int num_levels, const void* correction_seeds, const uint8_t* ccl,
+                               const uint8_t* ccr, const dpf_amd_value_type* vt,
+                               const int8_t* key_party, const void* key_value_corrections,
+                               void* out, void* stream);
+
 }  // namespace dpf_amd

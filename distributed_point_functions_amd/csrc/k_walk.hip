@@ -86,7 +86,8 @@ __device__ __forceinline__ void WalkPoints(const WalkArgs& w, Walk<NP>& s, const
     if (w.paths) {
       p[n] = w.paths[s.idx[n]];
     } else {  // implicit paths: point j of each key is tree index j
-      const uint64_t j = (uint64_t)(ppk > 0 ? s.idx[n] - s.src[n] * ppk : s.idx[n]);
+      const uint64_t j = (uint64_t)(ppk > 0 ? s.idx[n] - s.src[n] * ppk : s.idx[n]) +
+                         (uint64_t)w.path_offset;
       p[n] = make_uint4((uint32_t)j, (uint32_t)(j >> 32), 0u, 0u);
     }
   }

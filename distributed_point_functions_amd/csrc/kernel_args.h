@@ -64,6 +64,9 @@ struct WalkArgs {
   int64_t points_per_key;
   int32_t num_levels;
   int32_t rightshift;
+  // implicit paths (paths == nullptr): point j of each key walks tree index
+  // path_offset + j (a leaf range of a batched selection expansion)
+  int64_t path_offset;
 };
 
 struct PointsArgs {

@@ -194,6 +194,7 @@ int dpf_amd_evaluate_seeds(int64_t num_seeds, int num_levels, int64_t num_correc
     return rc;
   }
   WalkArgs a;
+  a.path_offset = 0;
   a.num_seeds = num_seeds;
   a.num_cw = num_correction_words;
   a.seeds_in = (const uint4*)seeds_in;
@@ -294,7 +295,7 @@ static int EvaluatePoints(int64_t num_points, int64_t points_per_key, int64_t nu
                           const uint8_t* block_index, const int8_t* party, int party_all,
                           const void* value_corrections, const uint64_t* value_correction_all,
                           void* out, void* seeds_out, uint8_t* control_bits_out,
-                          void* stream) {
+                          void* stream, int64_t path_offset = 0) {
   if (num_points < 0 || num_levels < 0 || !vt)
     return SetError(DPF_AMD_INVALID_ARGUMENT, "bad arguments");
   if (num_points == 0) return DPF_AMD_OK;
@@ -315,6 +316,7 @@ static int EvaluatePoints(int64_t num_points, int64_t points_per_key, int64_t nu
   a.w.points_per_key = points_per_key;
   a.w.num_levels = num_levels;
   a.w.rightshift = paths_rightshift;
+  a.w.path_offset = path_offset;
   a.block_index = block_index;
   a.party = party;
   a.value_corrections = (const uint4*)value_corrections;
@@ -362,6 +364,29 @@ int dpf_amd_evaluate_points_batched(int64_t num_keys, int64_t points_per_key,
                         key_value_corrections, value_correction_all, out, nullptr, nullptr,
                         stream);
 }
+
+}  // extern "C"
+
+namespace dpf_amd {
+int EvaluatePointsBatchedRange(int64_t num_keys, int64_t first_point, int64_t points_per_key,
+                               const void* key_seeds, const uint8_t* key_control_bits,
+                               int num_levels, const void* correction_seeds, const uint8_t* ccl,
+                               const uint8_t* ccr, const dpf_amd_value_type* vt,
+                               const int8_t* key_party, const void* key_value_corrections,
+                               void* out, void* stream) {
+  if (num_keys < 0 || points_per_key < 0 || first_point < 0)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "bad point range");
+  if (num_keys > 0 && points_per_key > INT64_MAX / num_keys)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "too many points");
+  if (num_keys == 0 || points_per_key == 0) return DPF_AMD_OK;
+  return EvaluatePoints(num_keys * points_per_key, points_per_key, num_keys * num_levels,
+                        key_seeds, key_control_bits, nullptr, 0, num_levels, correction_seeds,
+                        ccl, ccr, vt, nullptr, key_party, 0, key_value_corrections, nullptr, out,
+                        nullptr, nullptr, stream, first_point);
+}
+}  // namespace dpf_amd
+
+extern "C" {
 
 int dpf_amd_dcf_evaluate(int64_t num_keys, const void* seeds, const uint8_t* control_bits,
                          const int8_t* party, const void* points, int log_domain_size,

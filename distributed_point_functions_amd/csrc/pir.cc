@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <functional>
 
 #include "dpf_amd/dense_dpf_pir_server.h"
 #include "host_aes.h"
@@ -85,6 +86,31 @@ std::unique_ptr<DenseDpfPirDatabase::Interface::Builder> DenseDpfPirDatabase::Bu
   return r;
 }
 
+DenseDpfPirDatabase::Builder& DenseDpfPirDatabase::Builder::SetDevices(std::vector<int> devices) {
+  devices_ = std::move(devices);
+  return *this;
+}
+
+namespace {
+
+// Device allocation that first returns the pool's idle blocks on failure.
+Status MallocOrRelease(void** p, int64_t bytes) {
+  hipError_t e = hipMalloc(p, bytes);
+  if (e == hipErrorOutOfMemory) {
+    // idle blocks cached by earlier Tier-2 calls go back to the device first
+    (void)hipGetLastError();
+    dpf_internal_host::DevicePool::Get().Release();
+    e = hipMalloc(p, bytes);
+  }
+  return HipStatus(e, "hipMalloc(database)");
+}
+
+// Shard g of G over `blocks` 128-record selection blocks: blocks
+// [g * blocks / G, (g + 1) * blocks / G).
+int64_t ShardBlock(int64_t blocks, int64_t g, int64_t num) { return blocks * g / num; }
+
+}  // namespace
+
 StatusOr<std::unique_ptr<DenseDpfPirDatabase::Interface>> DenseDpfPirDatabase::Builder::Build() {
   if (has_been_built_) return FailedPreconditionError("Database already built");
   has_been_built_ = true;
@@ -97,62 +123,79 @@ StatusOr<std::unique_ptr<DenseDpfPirDatabase::Interface>> DenseDpfPirDatabase::B
   // Device row stride: the reference's 16-byte alignment (KPirScanG maps any
   // width onto the wave, so no padding is read or stored).
   db->stride_ = std::max<int64_t>(16, AlignBytes(max_size));
-  const int64_t bytes = std::max<int64_t>(16, n * db->stride_);
-  hipError_t e = hipMalloc(&db->records_, bytes);
-  if (e == hipErrorOutOfMemory) {
-    // idle blocks cached by earlier Tier-2 calls go back to the device first
-    (void)hipGetLastError();
-    dpf_internal_host::DevicePool::Get().Release();
-    e = hipMalloc(&db->records_, bytes);
+  std::vector<int> devices = devices_;
+  if (devices.empty()) {
+    int cur = 0;
+    DPF_RETURN_IF_ERROR(HipStatus(hipGetDevice(&cur), "hipGetDevice"));
+    devices.push_back(cur);
   }
-  DPF_RETURN_IF_ERROR(HipStatus(e, "hipMalloc(database)"));
-  DPF_RETURN_IF_ERROR(HipStatus(hipMemset(db->records_, 0, bytes), "hipMemset(database)"));
-  // Upload in 64 MiB chunks of zero-padded fixed-stride rows.
+  const int64_t blocks = (n + 127) / 128;
+  const int64_t num = static_cast<int64_t>(devices.size());
+  for (int64_t g = 0; g < num; ++g) {
+    const int64_t r0 = std::min(n, 128 * ShardBlock(blocks, g, num));
+    const int64_t r1 = std::min(n, 128 * ShardBlock(blocks, g + 1, num));
+    if (r1 > r0 || (g == 0 && n == 0)) db->shards_.push_back(Shard{devices[g], r0, r1, nullptr});
+  }
+  for (const Shard& a : db->shards_)  // peer access for the partials' combine copies
+    for (const Shard& b : db->shards_)
+      if (a.device != b.device) {
+        dpf_internal_host::DeviceGuard g(a.device);
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, a.device, b.device) == hipSuccess && can)
+          (void)hipDeviceEnablePeerAccess(b.device, 0);
+        (void)hipGetLastError();  // "already enabled" is not an error here
+      }
+  // Upload each shard in 64 MiB chunks of zero-padded fixed-stride rows.
   const int64_t rows_per_chunk = std::max<int64_t>(1, (64 << 20) / db->stride_);
   std::vector<char> chunk(rows_per_chunk * db->stride_);
-  int64_t row = 0;
-  auto flush = [&](int64_t rows) -> Status {
-    if (rows == 0) return OkStatus();
-    Status s = HipStatus(hipMemcpy(static_cast<char*>(db->records_) + (row - rows) * db->stride_,
-                                   chunk.data(), rows * db->stride_, hipMemcpyHostToDevice),
-                         "upload database");
-    std::fill(chunk.begin(), chunk.end(), 0);
-    return s;
-  };
-  int64_t in_chunk = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    const char* src;
-    int64_t len;
+  auto record = [&](int64_t i, const char** src, int64_t* len) {
     if (i < static_cast<int64_t>(values_.size())) {
-      src = values_[i].data();
-      len = static_cast<int64_t>(values_[i].size());
+      *src = values_[i].data();
+      *len = static_cast<int64_t>(values_[i].size());
     } else {
-      const int64_t j = i - static_cast<int64_t>(values_.size());
-      src = fixed_.data() + j * fixed_size_;
-      len = fixed_size_;
+      *src = fixed_.data() + (i - static_cast<int64_t>(values_.size())) * fixed_size_;
+      *len = fixed_size_;
     }
-    memcpy(chunk.data() + in_chunk * db->stride_, src, len);
-    ++in_chunk;
-    ++row;
-    if (in_chunk == rows_per_chunk) {
-      DPF_RETURN_IF_ERROR(flush(in_chunk));
-      in_chunk = 0;
+  };
+  for (Shard& sh : db->shards_) {
+    dpf_internal_host::DeviceGuard g(sh.device);
+    const int64_t bytes = std::max<int64_t>(16, (sh.row_end - sh.row_begin) * db->stride_);
+    DPF_RETURN_IF_ERROR(MallocOrRelease(&sh.records, bytes));
+    DPF_RETURN_IF_ERROR(HipStatus(hipMemset(sh.records, 0, bytes), "hipMemset(database)"));
+    for (int64_t r = sh.row_begin; r < sh.row_end; r += rows_per_chunk) {
+      const int64_t rows = std::min(rows_per_chunk, sh.row_end - r);
+      std::fill(chunk.begin(), chunk.end(), 0);
+      for (int64_t k = 0; k < rows; ++k) {
+        const char* src;
+        int64_t len;
+        record(r + k, &src, &len);
+        memcpy(chunk.data() + k * db->stride_, src, len);
+      }
+      DPF_RETURN_IF_ERROR(HipStatus(
+          hipMemcpy(static_cast<char*>(sh.records) + (r - sh.row_begin) * db->stride_,
+                    chunk.data(), rows * db->stride_, hipMemcpyHostToDevice),
+          "upload database"));
     }
   }
-  DPF_RETURN_IF_ERROR(flush(in_chunk));
   std::vector<std::string>().swap(values_);
   std::vector<char>().swap(fixed_);
   return std::unique_ptr<Interface>(std::move(db));
 }
 
 DenseDpfPirDatabase::~DenseDpfPirDatabase() {
-  if (records_) (void)hipFree(records_);
+  for (Shard& sh : shards_)
+    if (sh.records) {
+      dpf_internal_host::DeviceGuard g(sh.device);
+      (void)hipFree(sh.records);
+    }
 }
 
 StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductWithDevice(
     const void* selections_dev, int64_t selection_blocks, int num_queries, void* stream) const {
   if (num_queries == 0) return std::vector<std::string>();
   if (max_value_size_ <= 0) return InvalidArgumentError("`max_value_size` must be positive");
+  if (shards_.size() != 1)
+    return FailedPreconditionError("InnerProductWithDevice needs a single-shard database");
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : PirStream();
   const int64_t ws = dpf_amd_inner_product_workspace_size(num_records_, stride_, num_queries);
   void* work = nullptr;
@@ -161,8 +204,9 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductWithDevice(
   Status st = dpf_internal_host::DevicePool::Get().Alloc(num_queries * stride_, s, &out);
   std::vector<char> host(num_queries * stride_);
   if (st.ok())
-    st = AbiStatus(dpf_amd_inner_product(records_, num_records_, stride_, selections_dev,
-                                         selection_blocks, num_queries, work, out, s));
+    st = AbiStatus(dpf_amd_inner_product(shards_[0].records, num_records_, stride_,
+                                         selections_dev, selection_blocks, num_queries, work, out,
+                                         s));
   if (st.ok())
     st = HipStatus(hipMemcpyAsync(host.data(), out, host.size(), hipMemcpyDeviceToHost, s), "d2h");
   dpf_internal_host::DevicePool::Get().Free(work, s);
@@ -170,6 +214,113 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductWithDevice(
   Status sync = HipStatus(hipStreamSynchronize(s), "sync");
   if (!st.ok()) return st;
   if (!sync.ok()) return sync;
+  std::vector<std::string> r(num_queries);
+  for (int q = 0; q < num_queries; ++q) r[q].assign(host.data() + q * stride_, max_value_size_);
+  return r;
+}
+
+StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
+    const FillSelectionsFn& fill, int num_queries) const {
+  using dpf_internal_host::DeviceGuard;
+  using dpf_internal_host::DevicePool;
+  if (num_queries == 0) return std::vector<std::string>();
+  if (max_value_size_ <= 0) return InvalidArgumentError("`max_value_size` must be positive");
+  const size_t G = shards_.size();
+  const int64_t part_bytes = static_cast<int64_t>(num_queries) * stride_;
+  struct Work {
+    hipStream_t s = nullptr;
+    void* sel = nullptr;
+    void* ws = nullptr;
+    void* part = nullptr;
+    hipEvent_t done = nullptr;
+  };
+  std::vector<Work> w(G);
+  const int dev0 = shards_[0].device;
+  hipStream_t s0 = dpf_internal_host::ThreadStreamOn(dev0);
+  void* gather = nullptr;
+  void* folded = nullptr;
+  std::vector<char> host(part_bytes);
+  Status st = OkStatus();
+  // 1. every shard: its selection blocks, then its scan, on its own device
+  for (size_t g = 0; g < G && st.ok(); ++g) {
+    const Shard& sh = shards_[g];
+    DeviceGuard dg(sh.device);
+    Work& x = w[g];
+    x.s = dpf_internal_host::ThreadStreamOn(sh.device);
+    if (x.s == nullptr) {
+      st = InternalError("no stream on device " + std::to_string(sh.device));
+      break;
+    }
+    const int64_t b0 = sh.row_begin / 128, b1 = (sh.row_end + 127) / 128;
+    const int64_t nb = std::max<int64_t>(1, b1 - b0);
+    const int64_t rows = sh.row_end - sh.row_begin;
+    st = DevicePool::Get().Alloc(16 * nb * num_queries, x.s, &x.sel);
+    if (st.ok()) st = fill(sh, b0, b1, x.sel, x.s);
+    if (st.ok())
+      st = DevicePool::Get().Alloc(
+          std::max<int64_t>(16, dpf_amd_inner_product_workspace_size(rows, stride_, num_queries)),
+          x.s, &x.ws);
+    if (st.ok()) st = DevicePool::Get().Alloc(part_bytes, x.s, &x.part);
+    if (st.ok())
+      st = AbiStatus(dpf_amd_inner_product(sh.records, rows, stride_, x.sel, nb, num_queries,
+                                           x.ws, x.part, x.s));
+    if (st.ok() && G > 1) {
+      st = HipStatus(hipEventCreateWithFlags(&x.done, hipEventDisableTiming), "hipEventCreate");
+      if (st.ok()) st = HipStatus(hipEventRecord(x.done, x.s), "hipEventRecord");
+    }
+  }
+  // 2. combine on the first shard's device: peer copies of the partials,
+  // one XOR fold, one D2H
+  const void* result = nullptr;
+  if (st.ok()) {
+    DeviceGuard dg(dev0);
+    if (G == 1) {
+      result = w[0].part;
+    } else {
+      st = DevicePool::Get().Alloc(part_bytes * G, s0, &gather);
+      if (st.ok()) st = DevicePool::Get().Alloc(part_bytes, s0, &folded);
+      for (size_t g = 0; g < G && st.ok(); ++g) {
+        char* dst = static_cast<char*>(gather) + g * part_bytes;
+        st = HipStatus(hipStreamWaitEvent(s0, w[g].done, 0), "hipStreamWaitEvent");
+        if (!st.ok()) break;
+        if (shards_[g].device == dev0)
+          st = HipStatus(hipMemcpyAsync(dst, w[g].part, part_bytes, hipMemcpyDeviceToDevice, s0),
+                         "partials copy");
+        else
+          st = HipStatus(hipMemcpyPeerAsync(dst, dev0, w[g].part, shards_[g].device, part_bytes,
+                                            s0),
+                         "partials peer copy");
+      }
+      if (st.ok())
+        st = AbiStatus(dpf_amd_xor_fold(gather, static_cast<int>(G), part_bytes, folded, s0));
+      result = folded;
+    }
+    if (st.ok())
+      st = HipStatus(hipMemcpyAsync(host.data(), result, part_bytes, hipMemcpyDeviceToHost,
+                                    G == 1 ? w[0].s : s0),
+                     "d2h");
+  }
+  // 3. drain every stream used, then return the buffers (no copy still reads them)
+  for (size_t g = 0; g < G; ++g) {
+    if (!w[g].s) continue;
+    DeviceGuard dg(shards_[g].device);
+    Status sy = HipStatus(hipStreamSynchronize(w[g].s), "sync");
+    if (st.ok()) st = sy;
+  }
+  {
+    DeviceGuard dg(dev0);
+    Status sy = HipStatus(hipStreamSynchronize(s0), "sync");
+    if (st.ok()) st = sy;
+    if (gather) DevicePool::Get().Free(gather, s0);
+    if (folded) DevicePool::Get().Free(folded, s0);
+  }
+  for (size_t g = 0; g < G; ++g) {
+    DeviceGuard dg(shards_[g].device);
+    for (void* p : {w[g].sel, w[g].ws, w[g].part})
+      if (p) DevicePool::Get().Free(p, w[g].s);
+    if (w[g].done) (void)hipEventDestroy(w[g].done);
+  }
+  if (!st.ok()) return st;
   std::vector<std::string> r(num_queries);
   for (int q = 0; q < num_queries; ++q) r[q].assign(host.data() + q * stride_, max_value_size_);
   return r;
@@ -193,23 +344,20 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductWith(
                                   std::to_string(first));
     if (max_value_size_ <= 0) return InvalidArgumentError("`max_value_size` must be positive");
   }
-  // Only the blocks that select existing records are read by the scan.
-  const int64_t blocks = std::max<int64_t>(1, (num_records_ + 127) / 128);
+  // Only the blocks that select existing records are read by the scan: each
+  // shard gets its own blocks of every query, query-major.
   const int q = static_cast<int>(selections.size());
-  std::vector<uint128> host(static_cast<size_t>(q) * blocks);
-  for (int k = 0; k < q; ++k)
-    for (int64_t b = 0; b < blocks && b < static_cast<int64_t>(first); ++b)
-      host[k * blocks + b] = selections[k][b].value();
-  hipStream_t s = PirStream();
-  void* dev = nullptr;
-  DPF_RETURN_IF_ERROR(dpf_internal_host::DevicePool::Get().Alloc(16 * host.size(), s, &dev));
-  Status st = HipStatus(hipMemcpyAsync(dev, host.data(), 16 * host.size(),
-                                       hipMemcpyHostToDevice, s), "h2d");
-  StatusOr<std::vector<std::string>> r =
-      st.ok() ? InnerProductWithDevice(dev, blocks, q, s) : StatusOr<std::vector<std::string>>(st);
-  dpf_internal_host::DevicePool::Get().Free(dev, s);
-  (void)hipStreamSynchronize(s);
-  return r;
+  auto fill = [&](const Shard&, int64_t b0, int64_t b1, void* dev, void* stream) -> Status {
+    const int64_t nb = std::max<int64_t>(1, b1 - b0);
+    std::vector<uint128> host(static_cast<size_t>(q) * nb);
+    for (int k = 0; k < q; ++k)
+      for (int64_t b = b0; b < b1 && b < static_cast<int64_t>(first); ++b)
+        host[k * nb + (b - b0)] = selections[k][b].value();
+    // host is a local: copied through the pinned ring (async, safe to return)
+    return dpf_internal_host::ThreadUploadRing().Copy(dev, host.data(), 16 * host.size(),
+                                                     static_cast<hipStream_t>(stream));
+  };
+  return InnerProductSharded(fill, q);
 }
 
 // ---------------------------------------------------------------------------
@@ -378,27 +526,22 @@ StatusOr<PirResponse> DenseDpfPirServer::HandlePlainRequest(const PirRequest& re
   std::vector<std::string> inner_products;
   const auto* gpu_db = dynamic_cast<const DenseDpfPirDatabase*>(database_.get());
   if (gpu_db != nullptr) {
-    // Fused path: expand only the ceil(N/128) selection blocks the scan
-    // reads, straight into HBM, then scan.
+    // Fused path: expand only the selection blocks the scan reads, straight
+    // into HBM, then scan; a sharded database expands each shard's blocks
+    // (a leaf range of every key) on the shard's device.
     for (int i = 0; i < q; ++i) {
       StatusOr<EvaluationContext> ctx = dpf_->CreateEvaluationContext(plain.dpf_key(i));
       if (!ctx.ok()) return ctx.status();
     }
-    const int64_t n = static_cast<int64_t>(database_->size());
-    const int64_t blocks = std::max<int64_t>(1, (n + 127) / 128);
-    hipStream_t s = PirStream();
-    void* sel = nullptr;
-    DPF_RETURN_IF_ERROR(dpf_internal_host::DevicePool::Get().Alloc(16 * blocks * q, s, &sel));
     const dpf_amd_value_type layout = dpf_internal::HostLayoutOf<XorWrapper<uint128>>();
     std::vector<const DpfKey*> keys(q);
     for (int i = 0; i < q; ++i) keys[i] = &plain.dpf_key(i);
-    Status st = dpf_->ExpandLeavesOnDeviceBatched(
-        Span<const DpfKey* const>(keys.data(), keys.size()), blocks, layout, sel, s);
-    StatusOr<std::vector<std::string>> r =
-        st.ok() ? gpu_db->InnerProductWithDevice(sel, blocks, q, s)
-                : StatusOr<std::vector<std::string>>(st);
-    dpf_internal_host::DevicePool::Get().Free(sel, s);
-    (void)hipStreamSynchronize(s);
+    auto fill = [&](const DenseDpfPirDatabase::Shard&, int64_t b0, int64_t b1, void* sel,
+                    void* stream) -> Status {
+      return dpf_->ExpandLeavesOnDeviceBatched(Span<const DpfKey* const>(keys.data(), keys.size()),
+                                               b0, std::max(b1, b0 + 1), layout, sel, stream);
+    };
+    StatusOr<std::vector<std::string>> r = gpu_db->InnerProductSharded(fill, q);
     if (!r.ok()) return r.status();
     inner_products = std::move(*r);
   } else {

@@ -290,6 +290,22 @@ class DistributedPointFunction:
         return self.evaluate_until(ctx.previous_hierarchy_level + 1, prefixes, ctx,
                                    value_type, raw, out)
 
+    def expand_leaves_on_devices(self, key: DpfKey, slices) -> None:
+        """One key's last-level leaves over devices
+        (DistributedPointFunction::ExpandLeavesOnDevices): `slices` =
+        [(device, leaf_begin, leaf_end, out)] with `out` a device tensor (or
+        pointer) on that device holding (leaf_end - leaf_begin) elements in
+        the host layout; returns when every device is done."""
+        n = len(slices)
+        data = bytes(key)
+        devs = (ctypes.c_int * max(n, 1))(*[s[0] for s in slices])
+        lo = (ctypes.c_int64 * max(n, 1))(*[s[1] for s in slices])
+        hi = (ctypes.c_int64 * max(n, 1))(*[s[2] for s in slices])
+        outs = (ctypes.c_void_p * max(n, 1))(
+            *[s[3].data_ptr() if hasattr(s[3], "data_ptr") else s[3] for s in slices])
+        check(_lib.lib().dpf_amd_expand_leaves_on_devices(self._h, data, len(data), n, devs,
+                                                          lo, hi, outs))
+
     def evaluate_at(self, key: DpfKey, hierarchy_level: int, points: Sequence[int],
                     value_type: ValueType = None, raw: bool = False):
         """EvaluateAt<T>(key, level, points) (h:349-354)."""

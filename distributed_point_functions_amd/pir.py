@@ -9,7 +9,7 @@ protos in wire format (pir/private_information_retrieval.proto:62-151).
 from __future__ import annotations
 
 import ctypes
-from typing import Callable, List, Optional, Sequence
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -64,11 +64,17 @@ class DenseDpfPirDatabase:
     """DenseDpfPirDatabase::Builder + the built, HBM-resident database
     (pir/dense_dpf_pir_database.h:41-95)."""
 
-    def __init__(self):
+    def __init__(self, devices: Optional[Sequence[int]] = None):
+        """`devices`: shard the records over these devices (128-record-aligned
+        row ranges, one per entry; entries may repeat), see
+        dpf_amd_pir_db_set_devices. None: one shard on the current device."""
         h = ctypes.c_void_p()
         check(_lib.lib().dpf_amd_pir_db_create(ctypes.byref(h)))
         self._h = h
         self._owned = True
+        if devices:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            check(_lib.lib().dpf_amd_pir_db_set_devices(self._h, arr, len(devices)))
 
     def __del__(self):
         try:
@@ -99,6 +105,16 @@ class DenseDpfPirDatabase:
     @property
     def max_value_size(self) -> int:
         return _lib.lib().dpf_amd_pir_db_max_value_size(self._h)
+
+    def shards(self) -> List[Tuple[int, int, int]]:
+        """[(device, row_begin, row_end)] of the built database."""
+        out = []
+        for i in range(_lib.lib().dpf_amd_pir_db_num_shards(self._h)):
+            d, r0, r1 = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64()
+            check(_lib.lib().dpf_amd_pir_db_shard(self._h, i, ctypes.byref(d), ctypes.byref(r0),
+                                                  ctypes.byref(r1), None))
+            out.append((d.value, r0.value, r1.value))
+        return out
 
     @property
     def record_stride(self) -> int:

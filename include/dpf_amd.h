@@ -329,6 +329,17 @@ int dpf_amd_evaluate_until_device(const dpf_amd_dpf* dpf, int hierarchy_level,
                                   int64_t out_capacity, int64_t* num_outputs,
                                   void* stream);
 
+/* One key's full-domain leaves spread over devices (the c5 shape of
+ * DistributedPointFunction::ExpandLeavesOnDevices): slice i expands leaves
+ * [leaf_begin[i], leaf_end[i]) of the last hierarchy level, in the host
+ * layout of its value type, into device memory outs[i] on device
+ * devices[i]; all slices run concurrently (one stream per device of the
+ * calling thread) and the call returns when all are done. */
+int dpf_amd_expand_leaves_on_devices(const dpf_amd_dpf* dpf, const uint8_t* key,
+                                     size_t key_len, int num_slices,
+                                     const int* devices, const int64_t* leaf_begin,
+                                     const int64_t* leaf_end, void* const* outs);
+
 /* EvaluateAt<T>(key, level, points) (h:349-354, 913-1070). */
 int dpf_amd_evaluate_at(const dpf_amd_dpf* dpf, const uint8_t* key,
                         size_t key_len, int hierarchy_level,
@@ -388,7 +399,22 @@ int dpf_amd_pir_db_build(dpf_amd_pir_db* db);
 void dpf_amd_pir_db_destroy(dpf_amd_pir_db* db);
 int64_t dpf_amd_pir_db_size(const dpf_amd_pir_db* db);
 int64_t dpf_amd_pir_db_max_value_size(const dpf_amd_pir_db* db);
-/* Device pointer / stride of the resident records (bench, multi-GPU). */
+/* Shards the records over devices before dpf_amd_pir_db_build: contiguous
+ * row ranges aligned to 128-record selection blocks, one per entry of
+ * `devices` (entries may repeat). HandleRequest / InnerProductWith then scan
+ * every shard on its device and combine the Q x record partials on the first
+ * shard's device (peer copies over xGMI + one XOR fold). No call, or
+ * num_devices = 0: one shard on the current device. */
+int dpf_amd_pir_db_set_devices(dpf_amd_pir_db* db, const int* devices,
+                               int num_devices);
+int dpf_amd_pir_db_num_shards(const dpf_amd_pir_db* db);
+/* Shard `shard` of a built database: device, rows [row_begin, row_end),
+ * device pointer of its records (record stride: dpf_amd_pir_db_device_records).
+ * Any output pointer may be NULL. */
+int dpf_amd_pir_db_shard(const dpf_amd_pir_db* db, int shard, int* device,
+                         int64_t* row_begin, int64_t* row_end,
+                         const void** records);
+/* Device pointer / stride of the resident records of shard 0 (bench). */
 const void* dpf_amd_pir_db_device_records(const dpf_amd_pir_db* db,
                                           int64_t* record_stride);
 /* PirDatabaseInterface::InnerProductWith (pir/pir_database_interface.h:65-66):

@@ -61,6 +61,11 @@ class DenseDpfPirDatabase : public PirDatabaseInterface<XorWrapper<uint128>, std
     std::unique_ptr<PirDatabaseInterface::Builder> Clone() const override;
     StatusOr<std::unique_ptr<PirDatabaseInterface>> Build() override;
     int64_t total_database_bytes() const { return total_database_bytes_; }
+    // Devices the records are sharded over: contiguous row ranges aligned to
+    // the 128-record selection blocks, one per entry, in order (entries may
+    // repeat: {0, 0, 0, 0} is four shards on device 0).  Empty (default):
+    // one shard on the current device.
+    Builder& SetDevices(std::vector<int> devices);
 
    private:
     std::vector<std::string> values_;
@@ -68,6 +73,15 @@ class DenseDpfPirDatabase : public PirDatabaseInterface<XorWrapper<uint128>, std
     int64_t fixed_count_ = 0, fixed_size_ = 0;
     int64_t total_database_bytes_ = 0;
     bool has_been_built_ = false;
+    std::vector<int> devices_;
+  };
+
+  // Rows [row_begin, row_end) on `device` (selection blocks row_begin / 128
+  // up to ceil(row_end / 128)), stored at `records` with the database stride.
+  struct Shard {
+    int device;
+    int64_t row_begin, row_end;
+    void* records;
   };
 
   ~DenseDpfPirDatabase() override;
@@ -77,18 +91,32 @@ class DenseDpfPirDatabase : public PirDatabaseInterface<XorWrapper<uint128>, std
       Span<const std::vector<BlockType>> selections) const override;
   size_t max_value_size_in_bytes() const { return static_cast<size_t>(max_value_size_); }
 
-  // Device-side inner product: `selections_dev` holds num_queries *
-  // selection_blocks 128-bit blocks in HBM; returns host strings.
+  // Device-side inner product of a single-shard database: `selections_dev`
+  // holds num_queries * selection_blocks 128-bit blocks in HBM; returns host
+  // strings.
   StatusOr<std::vector<std::string>> InnerProductWithDevice(const void* selections_dev,
                                                             int64_t selection_blocks,
                                                             int num_queries,
                                                             void* stream) const;
-  const void* device_records() const { return records_; }
+  // Sharded inner product: for every shard, `fill(shard, block_begin,
+  // block_end, selections_dev, stream)` writes the num_queries x (block_end -
+  // block_begin) selection blocks of the shard's rows (query-major) into
+  // device memory on the shard's device, stream-ordered on `stream` (that
+  // device's stream of the calling thread); each shard is scanned there, and
+  // the num_queries x record partials of all shards are copied to the first
+  // shard's device (peer copies over xGMI) and XOR-folded (KXorFold).
+  using FillSelectionsFn = std::function<Status(const Shard& shard, int64_t block_begin,
+                                                int64_t block_end, void* selections_dev,
+                                                void* stream)>;
+  StatusOr<std::vector<std::string>> InnerProductSharded(const FillSelectionsFn& fill,
+                                                         int num_queries) const;
+  const std::vector<Shard>& shards() const { return shards_; }
+  const void* device_records() const { return shards_.empty() ? nullptr : shards_[0].records; }
   int64_t record_stride() const { return stride_; }
 
  private:
   DenseDpfPirDatabase() = default;
-  void* records_ = nullptr;
+  std::vector<Shard> shards_;
   int64_t num_records_ = 0;
   int64_t stride_ = 16;
   int64_t max_value_size_ = 0;

@@ -242,6 +242,20 @@ class DistributedPointFunction {
   Status ExpandLeavesOnDeviceBatched(Span<const DpfKey* const> keys, int64_t num_leaves,
                                      const dpf_amd_value_type& vt, void* out,
                                      void* stream) const;
+  // Leaves [leaf_begin, leaf_end) of every key, key i's at out + i *
+  // (leaf_end - leaf_begin) * cepb * out_stride (one database shard's
+  // selection blocks).
+  Status ExpandLeavesOnDeviceBatched(Span<const DpfKey* const> keys, int64_t leaf_begin,
+                                     int64_t leaf_end, const dpf_amd_value_type& vt, void* out,
+                                     void* stream) const;
+  // One key's leaves spread over devices: slice i expands leaves
+  // [leaf_begin[i], leaf_end[i]) on device devices[i] into that device's
+  // memory outs[i], each on the calling thread's stream for the device; all
+  // slices are issued before any is waited for, and the call returns when
+  // every device is done (c5 subtree-sharded over the GPUs of one process).
+  Status ExpandLeavesOnDevices(const DpfKey& key, Span<const int> devices,
+                               Span<const int64_t> leaf_begin, Span<const int64_t> leaf_end,
+                               Span<void* const> outs, const dpf_amd_value_type& vt) const;
 
  private:
   explicit DistributedPointFunction(std::unique_ptr<dpf_internal::DpfState> state);

@@ -258,3 +258,33 @@ def test_c4_full_size_handle_request_reconstructs(c4_db):
     r1 = P.parse_response(servers[1].handle_request(P.pir_request_plain([b for _, b in pairs])))
     for i, a, b in zip(idx, r0, r1):
         assert bytes(x ^ y for x, y in zip(a, b)) == c4_db["host"][i].tobytes(), i
+
+
+def test_c4_full_size_handle_request_on_sharded_database(c4_db):
+    """c4 through the library's multi-GPU path (rows in 8 shards, here all on
+    this GPU): the server's responses equal the single-shard server's bit for
+    bit, and the two parties' shares reconstruct the records."""
+    from distributed_point_functions_amd import pir as P
+    from distributed_point_functions_amd import value_types as V
+    from distributed_point_functions_amd.dpf import DistributedPointFunction, DpfParameters
+    sharded = P.DenseDpfPirDatabase([0] * 8)
+    sharded.insert_fixed(c4_db["host"])
+    sharded.build()
+    sh = sharded.shards()
+    assert len(sh) == 8 and sh[-1][2] == N4 and all(r0 % 128 == 0 for _, r0, _ in sh)
+    plain = P.DenseDpfPirDatabase()
+    plain.insert_fixed(c4_db["host"])
+    plain.build()
+    s_sharded = P.DenseDpfPirServer.create_plain(N4, sharded)
+    s_plain = P.DenseDpfPirServer.create_plain(N4, plain)
+    dpf = DistributedPointFunction.create(DpfParameters(26, V.XorWrapper(128)))
+    rng = random.Random(2626)
+    idx = [0, N4 - 1, (N4 // 8) - 1, N4 // 8] + [rng.randrange(N4) for _ in range(4)]
+    pairs = P.client_keys(dpf, N4, idx)
+    req0 = P.pir_request_plain([a for a, _ in pairs])
+    req1 = P.pir_request_plain([b for _, b in pairs])
+    r0 = P.parse_response(s_sharded.handle_request(req0))
+    assert r0 == P.parse_response(s_plain.handle_request(req0))
+    r1 = P.parse_response(s_plain.handle_request(req1))
+    for i, a, b in zip(idx, r0, r1):
+        assert bytes(x ^ y for x, y in zip(a, b)) == c4_db["host"][i].tobytes(), i
