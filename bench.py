@@ -14,10 +14,18 @@ outputs, no collective on the data path; `value` = 2^32 leaves / the
 max-over-ranks step time (strong scaling).
 
 Secondary (`pir`): dense PIR config c4 — 2^26 records x 256 B, one query:
-the selection DPF (only the ceil(N/128) leaves the scan reads) + the XOR
-scan over the whole database; rows sharded over ranks, the Q x 256 B
-partials are all-gathered with RCCL and XOR-folded.  GB/s = database bytes /
-time per query.
+the Tier-1 selection expansion (only the ceil(N/128) leaves the scan reads)
++ the XOR scan over the whole database; rows sharded over ranks, the Q x 256
+B partials are all-gathered with RCCL and XOR-folded.  GB/s = database
+bytes / time per query.  `pir.handle_request` (one rank) times the
+reference API itself, DenseDpfPirServer::HandleRequest through the C ABI
+(wire decode, key validation, expansion, scan, response encode) at Q = 1, 8,
+64 — the batch shapes of pir/dense_dpf_pir_database_benchmark.cc:37-157.
+
+--in-process: one process drives all N GPUs through the library's own
+multi-GPU entry points (ExpandLeavesOnDevices for c5; a DenseDpfPirDatabase
+sharded over the N devices behind HandleRequest for c4) instead of one
+process per GPU.
 
 `cpu_baseline` times the oracle (the C restatement of the reference CPU
 algorithm, AES-NI) single-threaded on a bounded slice of the same workload.
@@ -225,9 +233,82 @@ def bench_pir(args, world, rank, device):
     ev[1].record()
     barrier(world)
     mq_ms = max_over_ranks(ev[0].elapsed_time(ev[1]) / args.steps, world)
-    del mws, msel
+    del mws, msel, mout, ws, sel
+    hr = None
+    if world == 1 and not args.skip_handle_request:
+        torch.cuda.empty_cache()
+        hr = bench_handle_request(args, n, rec, db, device)
     return dict(ok=ok, wall_s=wall, scan_ms=scan_ms, db_bytes=n * rec, per_gpu_bytes=per * rec,
-                records=n, mq=mq, mq_ms=mq_ms)
+                records=n, mq=mq, mq_ms=mq_ms, hr=hr)
+
+
+def bench_handle_request(args, n, rec, db_tensor, device, shard_devices=None,
+                         queries=(1, 8, 64)):
+    """DenseDpfPirServer::HandleRequest (pir/dense_dpf_pir_server.cc:92-127)
+    through the C ABI, end to end per request: PirRequest wire decode, key
+    validation, the selection expansion, the scan, PirResponse encode and the
+    copy of the response to the host.  The database is built from the
+    resident rows (device to device).  Returns {Q: ms per request}, and
+    whether both parties' responses reconstruct the record at Q = 1."""
+    from distributed_point_functions_amd import pir as P
+    db = P.DenseDpfPirDatabase(shard_devices)
+    db.insert_fixed_device(db_tensor, n, rec).build()
+    server = P.DenseDpfPirServer.create_plain(n, db)
+    log_domain = max(0, (n - 1).bit_length())
+    dpf = DistributedPointFunction.create(DpfParameters(log_domain, V.XorWrapper(128)))
+    rng = np.random.default_rng(77)
+    out, ok = {}, None
+    for q in queries:
+        idx = [int(i) for i in rng.integers(0, n, q)]
+        pairs = P.client_keys(dpf, n, idx, seeds=[(7 + 2 * j, 8 + 2 * j) for j in range(q)])
+        req0 = P.pir_request_plain([a for a, _ in pairs])
+        r0 = P.parse_response(server.handle_request(req0))  # warm-up
+        if ok is None:
+            r1 = P.parse_response(server.handle_request(
+                P.pir_request_plain([b for _, b in pairs])))
+            want = db_tensor[idx[0] * rec:(idx[0] + 1) * rec].cpu().numpy().tobytes()
+            ok = bytes(x ^ y for x, y in zip(r0[0], r1[0])) == want
+        reps = max(3, args.steps)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            server.handle_request(req0)
+        out[q] = 1e3 * (time.perf_counter() - t0) / reps
+    del server, db
+    return out, ok
+
+
+def bench_in_process(args):
+    """All N GPUs from one process through the library's multi-GPU API."""
+    from distributed_point_functions_amd import pir as P
+    ngpu = args.gpus
+    devs = list(range(ngpu))
+    vt = V.Tuple(V.Integer(32), V.IntModN(64, P64))
+    dpf = DistributedPointFunction.create(DpfParameters(args.log_domain, vt, 48))
+    alpha = 0x9E3779B9 % (1 << args.log_domain)
+    k0, _ = dpf.generate_keys(alpha, (123456789, 987654321), seeds=(0xA5A5, 0x5A5A))
+    total = 1 << dpf.hierarchy_to_tree(0)
+    slices = []
+    for r in devs:
+        lo, hi = sharding.block_range(total, ngpu, r)
+        slices.append((r, lo, hi, torch.empty((hi - lo) * 16, dtype=torch.uint8,
+                                              device=torch.device("cuda", r))))
+    for _ in range(args.warmup):
+        dpf.expand_leaves_on_devices(k0, slices)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dpf.expand_leaves_on_devices(k0, slices)  # returns when every GPU is done
+    wall = time.perf_counter() - t0
+    del slices
+    torch.cuda.empty_cache()
+    pir = None
+    if not args.skip_pir:
+        n, rec = 1 << args.pir_log_records, 256
+        gen = torch.Generator(device="cuda:0")
+        gen.manual_seed(1234)
+        src = torch.randint(0, 256, (n * rec,), dtype=torch.uint8, device="cuda:0", generator=gen)
+        hr, ok = bench_handle_request(args, n, rec, src, torch.device("cuda", 0), devs)
+        pir = dict(ms=hr, ok=ok, n=n, rec=rec)
+    return dict(wall=wall, leaves=total, L=dpf.hierarchy_to_tree(0), pir=pir)
 
 
 def library_sha256():
@@ -335,7 +416,13 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--skip-cpu-baseline", action="store_true")
     ap.add_argument("--skip-pir", action="store_true")
+    ap.add_argument("--skip-handle-request", action="store_true")
+    ap.add_argument("--in-process", action="store_true",
+                    help="drive all --gpus GPUs from this one process through the library's "
+                         "multi-GPU API (ExpandLeavesOnDevices, a sharded DenseDpfPirDatabase)")
     args = ap.parse_args()
+    if args.in_process:
+        return main_in_process(args)
     world, rank, device = setup()
     r = bench_dpf(args, world, rank, device)
     pir = None if args.skip_pir else bench_pir(args, world, rank, device)
@@ -384,13 +471,16 @@ def main():
                          # build) and the fraction against the LDS peak at it
                          "measured": (dict(clk, frac_at_measured_clock=(
                              lookups_s / (LDS_PEAK_LOOKUPS * clk["clock_ghz"] / 2.4)))
-                             if clk else None),
-                         # implementation-independent view:
-                         # a bitsliced AES needs 757.5 gate ops per block
-                         "valu_equivalent": {"ops_per_aes": OPS_PER_AES,
-                                             "achieved_tops": achieved,
-                                             "peak_tops": VALU_PEAK_TOPS,
-                                             "frac": achieved / VALU_PEAK_TOPS}},
+                             if clk else None)},
+            # Not a roofline: the implementation-independent reference point
+            # of SURVEY.md §8d — AES/s priced at the 757.5 two-input gate ops
+            # a bitsliced AES-128 needs per block, against the VALU issue
+            # rate.  This T-table kernel does not perform those ops (it does
+            # ~300 VALU + 160 LDS lookups per AES), so the ratio can exceed 1.
+            "bitsliced_equivalent": {"gate_ops_per_aes": OPS_PER_AES,
+                                     "equivalent_tops": achieved,
+                                     "valu_peak_tops": VALU_PEAK_TOPS,
+                                     "ratio_to_valu_peak": achieved / VALU_PEAK_TOPS},
             "cpu_baseline": cpu,
         }
         if pir is not None:
@@ -398,8 +488,8 @@ def main():
             scan_gbs = pir["per_gpu_bytes"] / (pir["scan_ms"] / 1e3) / 1e9
             out["pir"] = {
                 "metric": "dense-PIR scan GB/s", "value": gbs, "unit": "GB/s",
-                "workload": "c4: %d records x 256 B, Q=1, HandlePlainRequest path "
-                            "(selection DPF + XOR scan%s)" %
+                "workload": "c4: %d records x 256 B, Q=1, Tier-1 selection expansion + "
+                            "XOR scan%s (the reference API path is handle_request below)" %
                             (pir["records"], " + RCCL all-gather + fold" if world > 1 else ""),
                 "ms_per_query": 1e3 * pir["wall_s"], "correct": pir["ok"],
                 "scaling": "strong",
@@ -414,9 +504,42 @@ def main():
                     "db_GBps": pir["db_bytes"] / (pir["mq_ms"] / 1e3) / 1e9,
                     "kernel": "KPirScanM4<1>+KXorFold (scan only, no selection DPF)"},
             }
+            if pir.get("hr"):
+                hr, hr_ok = pir["hr"]
+                out["pir"]["handle_request"] = {
+                    "api": "DenseDpfPirServer::HandleRequest via dpf_amd_pir_server_handle_request "
+                           "(wire decode + validation + selection expansion + scan + encode + D2H)",
+                    "ms_per_request": {str(q): v for q, v in hr.items()},
+                    "db_GBps_at_q1": pir["db_bytes"] / (hr[1] / 1e3) / 1e9 if 1 in hr else None,
+                    "correct": hr_ok}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def main_in_process(args):
+    r = bench_in_process(args)
+    ms = 1000 * r["wall"] / args.steps
+    out = {
+        "metric": METRIC, "value": r["leaves"] / (r["wall"] / args.steps), "unit": "leaves/s",
+        "n_gpus": args.gpus, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "tuple<u32,intmodn<u64>>", "data": "synthetic (fixed-seed DPF key)",
+        "config": {"workload": "c5: full-domain expansion, log_domain_size=%d, "
+                               "Tuple<uint32,IntModN<uint64,2^64-59>>, security_parameter=48"
+                               % args.log_domain,
+                   "leaves_per_step": r["leaves"], "tree_levels": r["L"],
+                   "parallelism": "in-process: DistributedPointFunction::ExpandLeavesOnDevices "
+                                  "over %d GPU(s), disjoint subtree slices" % args.gpus},
+    }
+    if r["pir"]:
+        p = r["pir"]
+        out["pir"] = {"api": "DenseDpfPirServer::HandleRequest, database sharded over %d GPU(s)"
+                             % args.gpus,
+                      "ms_per_request": {str(q): v for q, v in p["ms"].items()},
+                      "db_GBps_at_q1": p["n"] * p["rec"] / (p["ms"][1] / 1e3) / 1e9,
+                      "correct": p["ok"]}
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

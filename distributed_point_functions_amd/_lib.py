@@ -158,6 +158,7 @@ def _bind_tier2(L):
     _sig(L, "dpf_amd_pir_db_device_records", P, P, ctypes.POINTER(I64))
     _sig(L, "dpf_amd_pir_db_inner_product", I32, P, P, I64, I32, P)
     _sig(L, "dpf_amd_pir_db_set_devices", I32, P, P, I32)
+    _sig(L, "dpf_amd_pir_db_insert_fixed_device", I32, P, P, I32, I64, I64)
     _sig(L, "dpf_amd_pir_db_num_shards", I32, P)
     _sig(L, "dpf_amd_pir_db_shard", I32, P, I32, ctypes.POINTER(ctypes.c_int),
          ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.POINTER(P))

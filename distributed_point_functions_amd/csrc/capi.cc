@@ -409,6 +409,15 @@ int dpf_amd_release_cached_memory(int64_t* released) {
   return DPF_AMD_OK;
 }
 
+int dpf_amd_pir_db_insert_fixed_device(dpf_amd_pir_db* db, const void* records, int device,
+                                       int64_t num_records, int64_t record_size) {
+  if (!db->builder) return Fail(DPF_AMD_FAILED_PRECONDITION, "Database already built");
+  if (num_records < 0 || record_size < 0 || (num_records > 0 && records == nullptr))
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "bad device records");
+  db->builder->InsertFixedFromDevice(records, device, num_records, record_size);
+  return DPF_AMD_OK;
+}
+
 int dpf_amd_pir_db_set_devices(dpf_amd_pir_db* db, const int* devices, int num_devices) {
   if (!db->builder) return Fail(DPF_AMD_FAILED_PRECONDITION, "Database already built");
   if (num_devices < 0 || (num_devices > 0 && devices == nullptr))

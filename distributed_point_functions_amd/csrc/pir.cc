@@ -49,6 +49,10 @@ int64_t AlignBytes(int64_t n) { return (n + 15) & ~int64_t{15}; }
 DenseDpfPirDatabase::Builder::Builder() = default;
 
 DenseDpfPirDatabase::Builder& DenseDpfPirDatabase::Builder::Insert(std::string value) {
+  if (device_records_ != nullptr) {
+    mixed_inserts_ = true;
+    return *this;
+  }
   if (fixed_count_ > 0) {  // keep insertion order: materialise bulk records first
     for (int64_t i = 0; i < fixed_count_; ++i)
       values_.emplace_back(fixed_.data() + i * fixed_size_, fixed_size_);
@@ -63,6 +67,10 @@ DenseDpfPirDatabase::Builder& DenseDpfPirDatabase::Builder::Insert(std::string v
 DenseDpfPirDatabase::Builder& DenseDpfPirDatabase::Builder::InsertFixed(const char* data,
                                                                         int64_t num,
                                                                         int64_t size) {
+  if (device_records_ != nullptr) {
+    mixed_inserts_ = true;
+    return *this;
+  }
   if (fixed_count_ == 0) fixed_size_ = size;
   if (!values_.empty() || size != fixed_size_) {
     for (int64_t i = 0; i < num; ++i) Insert(std::string(data + i * size, size));
@@ -83,7 +91,22 @@ std::unique_ptr<DenseDpfPirDatabase::Interface::Builder> DenseDpfPirDatabase::Bu
   r->fixed_size_ = fixed_size_;
   r->total_database_bytes_ = total_database_bytes_;
   r->has_been_built_ = has_been_built_;
+  r->devices_ = devices_;
+  r->device_records_ = device_records_;
+  r->device_of_records_ = device_of_records_;
+  r->mixed_inserts_ = mixed_inserts_;
   return r;
+}
+
+DenseDpfPirDatabase::Builder& DenseDpfPirDatabase::Builder::InsertFixedFromDevice(
+    const void* records, int device, int64_t num, int64_t size) {
+  if (!values_.empty() || fixed_count_ > 0 || device_records_ != nullptr) mixed_inserts_ = true;
+  device_records_ = records;
+  device_of_records_ = device;
+  fixed_count_ = num;
+  fixed_size_ = size;
+  total_database_bytes_ += num * AlignBytes(size);
+  return *this;
 }
 
 DenseDpfPirDatabase::Builder& DenseDpfPirDatabase::Builder::SetDevices(std::vector<int> devices) {
@@ -113,6 +136,8 @@ int64_t ShardBlock(int64_t blocks, int64_t g, int64_t num) { return blocks * g /
 
 StatusOr<std::unique_ptr<DenseDpfPirDatabase::Interface>> DenseDpfPirDatabase::Builder::Build() {
   if (has_been_built_) return FailedPreconditionError("Database already built");
+  if (mixed_inserts_)
+    return InvalidArgumentError("InsertFixedFromDevice must be the only insert of a database");
   has_been_built_ = true;
   std::unique_ptr<DenseDpfPirDatabase> db(new DenseDpfPirDatabase());
   const int64_t n = static_cast<int64_t>(values_.size()) + fixed_count_;
@@ -157,11 +182,34 @@ StatusOr<std::unique_ptr<DenseDpfPirDatabase::Interface>> DenseDpfPirDatabase::B
       *len = fixed_size_;
     }
   };
+  if (device_records_ != nullptr) {
+    // every kernel or copy that writes the source rows was issued before
+    // Build, on whatever stream: drain the source device first
+    dpf_internal_host::DeviceGuard g(device_of_records_);
+    DPF_RETURN_IF_ERROR(HipStatus(hipDeviceSynchronize(), "hipDeviceSynchronize"));
+  }
   for (Shard& sh : db->shards_) {
     dpf_internal_host::DeviceGuard g(sh.device);
     const int64_t bytes = std::max<int64_t>(16, (sh.row_end - sh.row_begin) * db->stride_);
     DPF_RETURN_IF_ERROR(MallocOrRelease(&sh.records, bytes));
     DPF_RETURN_IF_ERROR(HipStatus(hipMemset(sh.records, 0, bytes), "hipMemset(database)"));
+    if (device_records_ != nullptr) {
+      // records already in HBM: one (peer) copy per shard, rows re-strided
+      // to 16-byte alignment when the record size is not a multiple of 16
+      const char* src = static_cast<const char*>(device_records_) + sh.row_begin * fixed_size_;
+      const int64_t rows = sh.row_end - sh.row_begin;
+      if (rows == 0) continue;
+      if (fixed_size_ == db->stride_ && sh.device != device_of_records_)
+        DPF_RETURN_IF_ERROR(HipStatus(hipMemcpyPeer(sh.records, sh.device, src,
+                                                    device_of_records_, rows * fixed_size_),
+                                      "database peer copy"));
+      else
+        DPF_RETURN_IF_ERROR(HipStatus(
+            hipMemcpy2D(sh.records, db->stride_, src, fixed_size_, fixed_size_, rows,
+                        hipMemcpyDeviceToDevice),
+            "database device copy"));
+      continue;
+    }
     for (int64_t r = sh.row_begin; r < sh.row_end; r += rows_per_chunk) {
       const int64_t rows = std::min(rows_per_chunk, sh.row_end - r);
       std::fill(chunk.begin(), chunk.end(), 0);
@@ -177,8 +225,16 @@ StatusOr<std::unique_ptr<DenseDpfPirDatabase::Interface>> DenseDpfPirDatabase::B
           "upload database"));
     }
   }
+  // The copies above run on the null stream; the scans run on the library's
+  // non-blocking streams, which do not wait for it: the rows are complete
+  // on every shard device before the database is handed out.
+  for (const Shard& sh : db->shards_) {
+    dpf_internal_host::DeviceGuard g(sh.device);
+    DPF_RETURN_IF_ERROR(HipStatus(hipDeviceSynchronize(), "hipDeviceSynchronize"));
+  }
   std::vector<std::string>().swap(values_);
   std::vector<char>().swap(fixed_);
+  device_records_ = nullptr;
   return std::unique_ptr<Interface>(std::move(db));
 }
 

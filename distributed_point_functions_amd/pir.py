@@ -94,6 +94,15 @@ class DenseDpfPirDatabase:
                                                      a.shape[0], a.shape[1]))
         return self
 
+    def insert_fixed_device(self, records, num_records: int, record_size: int) -> "DenseDpfPirDatabase":
+        """Bulk insert of records already in device memory (a CUDA uint8
+        tensor of num_records * record_size bytes); copied device to device
+        at build time."""
+        check(_lib.lib().dpf_amd_pir_db_insert_fixed_device(
+            self._h, records.data_ptr(), records.device.index or 0, num_records, record_size))
+        self._device_src = records  # keep alive until build
+        return self
+
     def build(self) -> "DenseDpfPirDatabase":
         check(_lib.lib().dpf_amd_pir_db_build(self._h))
         return self

@@ -395,6 +395,12 @@ int dpf_amd_pir_db_insert(dpf_amd_pir_db* db, const uint8_t* record,
 /* Bulk insert of num_records records of equal size. */
 int dpf_amd_pir_db_insert_fixed(dpf_amd_pir_db* db, const uint8_t* records,
                                 int64_t num_records, int64_t record_size);
+/* Bulk insert of num_records records of record_size bytes that already live
+ * in device memory on `device` (consecutive); Build copies them device to
+ * device, never through the host. Must be the only insert of the database. */
+int dpf_amd_pir_db_insert_fixed_device(dpf_amd_pir_db* db, const void* records,
+                                       int device, int64_t num_records,
+                                       int64_t record_size);
 int dpf_amd_pir_db_build(dpf_amd_pir_db* db);
 void dpf_amd_pir_db_destroy(dpf_amd_pir_db* db);
 int64_t dpf_amd_pir_db_size(const dpf_amd_pir_db* db);

@@ -58,6 +58,11 @@ class DenseDpfPirDatabase : public PirDatabaseInterface<XorWrapper<uint128>, std
     Builder& Insert(std::string value) override;
     // Bulk insert of `num` records of `size` bytes each (fast path).
     Builder& InsertFixed(const char* data, int64_t num, int64_t size);
+    // Bulk insert of `num` records of `size` bytes each that already live in
+    // device memory on `device` (consecutive, `size` bytes apart): Build()
+    // copies them device-to-device (peer copies for shards elsewhere) and
+    // never stages them through the host.  Must be the only insert.
+    Builder& InsertFixedFromDevice(const void* records, int device, int64_t num, int64_t size);
     std::unique_ptr<PirDatabaseInterface::Builder> Clone() const override;
     StatusOr<std::unique_ptr<PirDatabaseInterface>> Build() override;
     int64_t total_database_bytes() const { return total_database_bytes_; }
@@ -74,6 +79,9 @@ class DenseDpfPirDatabase : public PirDatabaseInterface<XorWrapper<uint128>, std
     int64_t total_database_bytes_ = 0;
     bool has_been_built_ = false;
     std::vector<int> devices_;
+    const void* device_records_ = nullptr;  // InsertFixedFromDevice
+    int device_of_records_ = 0;
+    bool mixed_inserts_ = false;
   };
 
   // Rows [row_begin, row_end) on `device` (selection blocks row_begin / 128

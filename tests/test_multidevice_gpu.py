@@ -138,3 +138,20 @@ def test_expand_leaves_on_devices_matches_one_launch_and_oracle(cuda):
     want = od.evaluate_until_words(0, [], od.create_evaluation_context(ok0))
     got = full.cpu().numpy().view(np.uint64).reshape(-1, 2)
     assert np.array_equal(got[:, 0], want[:, 1, 0]) and np.array_equal(got[:, 1], want[:, 0, 0])
+
+
+@pytest.mark.parametrize("size,shards", [(256, None), (40, [0, 0, 0]), (1040, [0, 0])])
+def test_insert_fixed_device_equals_host_built(P, cuda, size, shards):
+    """A database built from rows already in HBM (written by a torch kernel
+    just before the build, on another stream than the library's) scans like
+    the host-built one, also re-strided (40 B rows -> 48 B) and sharded."""
+    import torch
+    n = 128 * 21 + 9
+    g = torch.Generator(device=cuda)
+    g.manual_seed(size)
+    rows = torch.randint(0, 256, (n * size,), dtype=torch.uint8, device=cuda, generator=g)
+    dev_db = P.DenseDpfPirDatabase(shards).insert_fixed_device(rows, n, size).build()
+    host_db = _db(P, rows.cpu().numpy().reshape(n, size))
+    rng = random.Random(size)
+    sels = _sel(rng, 6, n)
+    assert dev_db.inner_product_with(sels) == host_db.inner_product_with(sels)
