@@ -539,6 +539,11 @@ struct ExpandCtx {
   const ExpandArgs& a;
   const VtDev& vt;
   const Lds& L;
+  // batched keys: this block's key's packed value correction and party
+  // (EmitDirect); otherwise vt.corr_packed / vt.party apply
+  bool per_key = false;
+  uint32_t kcorr[4] = {0u, 0u, 0u, 0u};
+  int kparty = 0;
 };
 
 // Value PRG of one seed: block j = H_value(seed + j) (cc:523-547).

@@ -1684,6 +1684,44 @@ Status DistributedPointFunction::ExpandLeavesOnDeviceBatched(Span<const DpfKey* 
   const bool walk = q > 1 && cepb == 1 &&
                     static_cast<double>(q) * num_leaves * (L + 1) <= static_cast<double>(1 << 25);
   char* o = static_cast<char*>(out);
+  const bool single_direct = vt.directly_convertible && vt.num_scalars == 1 &&
+                             vt.scalars[0].in_offset == 0 && vt.scalars[0].out_offset == 0 &&
+                             vt.out_stride == vt.scalars[0].bytes && vt.blocks_needed == 1 &&
+                             vt.elements_per_block * vt.scalars[0].bytes == 16;
+  if (!walk && q > 1 && single_direct && L >= 11 && num_leaves < (int64_t{1} << 25)) {
+    // One launch for every key (KExpandCoop, batched): the tree of each key
+    // is computed once per 2^10-2^11-leaf block, all keys' blocks in one grid
+    // (a 64-key c4 request: one launch instead of 64 small ones).
+    const int64_t off_cw = 16 * q, off_corr = off_cw + 16 * q * L, off_cb = off_corr + 16 * q;
+    const int64_t off_party = off_cb + q, off_ccl = off_party + q, off_ccr = off_ccl + q * L;
+    std::vector<char> host(off_ccr + q * L + 16, 0);
+    std::vector<uint128> corr;
+    for (int64_t k = 0; k < q; ++k) {
+      const DpfKey& key = *keys[k];
+      const uint128 seed = MakeUint128(key.seed().high(), key.seed().low());
+      memcpy(host.data() + 16 * k, &seed, 16);
+      const CwArrays cw = KeyCws(key, 0, L);
+      memcpy(host.data() + off_cw + 16 * k * L, cw.seeds.data(), 16 * L);
+      memcpy(host.data() + off_ccl + k * L, cw.ccl.data(), L);
+      memcpy(host.data() + off_ccr + k * L, cw.ccr.data(), L);
+      DPF_RETURN_IF_ERROR(CorrectionsFor(st, key, h, &corr));
+      uint64_t packed[2];
+      DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd::PackedCorrection(
+          vt, reinterpret_cast<const uint64_t*>(corr.data()), cepb, packed)));
+      memcpy(host.data() + off_corr + 16 * k, packed, 16);
+      host[off_cb + k] = static_cast<char>(key.party() != 0);
+      host[off_party + k] = static_cast<char>(key.party());
+    }
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ThreadStream();
+    DeviceBuffer dev;
+    DPF_RETURN_IF_ERROR(dev.Upload(host.data(), host.size(), s));
+    char* d = dev.as<char>();
+    return AbiStatus(dpf_amd::ExpandBatched(
+        q, d, reinterpret_cast<const uint8_t*>(d + off_cb), L, d + off_cw,
+        reinterpret_cast<const uint8_t*>(d + off_ccl), reinterpret_cast<const uint8_t*>(d + off_ccr),
+        &vt, d + off_corr, reinterpret_cast<const int8_t*>(d + off_party), cepb, leaf_begin,
+        leaf_end, out, s));
+  }
   if (!walk) {
     for (int64_t i = 0; i < q; ++i)
       DPF_RETURN_IF_ERROR(ExpandLeavesOnDevice(*keys[i], leaf_begin, leaf_end, layout,

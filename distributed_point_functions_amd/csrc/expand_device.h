@@ -38,6 +38,7 @@ template <int BN>
 struct EmitGeneric {
   static constexpr int kBN = BN;
   static constexpr bool kCanStage = false;
+  static constexpr bool kCanBatch = false;
   __device__ static void Emit(const ExpandCtx& E, const uint32_t (&h)[BN][4], uint32_t t,
                               int64_t g) {
     const VtDev& vt = E.vt;
@@ -121,6 +122,7 @@ struct EmitDirect {
   static constexpr bool kCanStage = true;  // when Packed(vt)
   // Whole 16-byte blocks per leaf (every element of the block is returned).
   __device__ static bool Packed(const VtDev& vt) { return vt.cepb * B == 16; }
+  static constexpr bool kCanBatch = true;  // per-key corrections (ExpandCtx::per_key)
   __device__ static uint4 Value(const ExpandCtx& E, const uint32_t (&h)[1][4], uint32_t t) {
     const VtDev& vt = E.vt;
     uint32_t w[4], c[4];
@@ -128,14 +130,15 @@ struct EmitDirect {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       w[i] = h[0][i];
-      c[i] = (uint32_t)(vt.corr_packed >> (32 * i)) & m;
+      c[i] = (E.per_key ? E.kcorr[i] : (uint32_t)(vt.corr_packed >> (32 * i))) & m;
     }
+    const int party = E.per_key ? E.kparty : vt.party;
     if (vt.sc[0].kind == DPF_AMD_KIND_XOR_WRAPPER) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) w[i] ^= c[i];
     } else {
       SwarAdd<B>(w, c);
-      if (vt.party == 1) SwarNeg<B>(w);
+      if (party == 1) SwarNeg<B>(w);
     }
     return make_uint4(w[0], w[1], w[2], w[3]);
   }
@@ -162,6 +165,7 @@ struct EmitDirect {
 struct EmitU32ModN64 {
   static constexpr int kBN = 2;
   static constexpr bool kCanStage = true;  // when Packed(vt)
+  static constexpr bool kCanBatch = false;
   // libstdc++ tuple layout: u64 at 0, u32 at 8, stride 16.
   __device__ static bool Packed(const VtDev& vt) {
     return vt.sc[0].out_off == 8 && vt.sc[1].out_off == 0 && vt.stride == 16;
@@ -369,8 +373,165 @@ int LaunchExpand(int, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
   return LaunchCheck("expand kernel launch");
 }
 
+// ----------------------------------------------------------------------------
+// KExpandCoop<E, Em, kBatched>: cooperative expansion for launches below
+// 2^25 tree leaves and for batches of keys (the selection vectors of a PIR
+// request).  KExpand gives every thread its own walk from the root, which
+// small launches cannot amortise (a 2^19-leaf launch at D = 2: 27 AES per 4
+// leaves against 12, and a 17-AES chain per thread).  Here a block owns a
+// 2^(10+E)-leaf subtree and computes every tree node of it once:
+//   1. wave 0 walks from the root to the block root (block-uniform path
+//      bits: one AES per level with the key chosen on the scalar unit) and
+//      on to 64 sub-roots six levels below (per-lane bits: masked keys);
+//   2. four breadth-first levels through LDS, one child per thread (a walk
+//      step with the key of the child's side): 64 -> 128 -> ... -> 1024;
+//   3. each thread hashes its node (E = 0) or expands it once more and
+//      hashes both children (E = 1), converts, corrects and stores —
+//      consecutive threads write consecutive leaves.
+// Per 2^10 leaves (E = 0, BN = 1): (s + 6) + 30 + 16 wave-AES for 48
+// algorithmic, s = tree depth of the block root.
+// ----------------------------------------------------------------------------
+
+#ifndef DPF_COOP_BLOCK
+#define DPF_COOP_BLOCK 1024
+#endif
+#ifndef DPF_COOP_WAVES
+#define DPF_COOP_WAVES 8  // 2 blocks per CU (72 KiB LDS each)
+#endif
+constexpr int kCoopBlock = DPF_COOP_BLOCK;
+static_assert(kCoopBlock == 1024, "the BFS levels assume 1024 threads (64 -> 1024 nodes)");
+constexpr int kCoopLog = 10;  // log2 nodes after the BFS
+
+template <int E, class Em, bool kBatched>
+__global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(ExpandArgs a,
+                                                                          VtDev vt) {
+  __shared__ uint32_t tab[kTabWords];
+  __shared__ uint4 nodes[kCoopBlock / 2];
+  constexpr int BN = Em::kBN;
+  constexpr int K = kCoopLog + E;  // log2 tree leaves per block
+  FillTables(tab);
+  __syncthreads();
+  const Lds L = MakeLds(tab);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int64_t cpk = a.chunk_end - a.chunk_begin;  // blocks per key
+  const int64_t key = kBatched ? (int64_t)blockIdx.x / cpk : 0;
+  const int64_t chunk = a.chunk_begin + (kBatched ? (int64_t)blockIdx.x % cpk : blockIdx.x);
+  const int s = a.walk;  // tree depth of the block root (below its root seed)
+  const int64_t root = kBatched ? key : chunk >> s;
+  const uint64_t path = (uint64_t)chunk & ((s >= 63) ? ~0ull : ((1ull << s) - 1));
+  const int64_t cw0 = kBatched ? key * a.num_levels : 0;
+  // 1. root -> block root -> 64 sub-roots (wave 0)
+  if (wave == 0) {
+    const uint4 rs = a.root_seeds[root];
+    uint32_t x[4] = {rs.x, rs.y, rs.z, rs.w};
+    uint32_t t = a.root_cb[root];
+    for (int i = 0; i < s; ++i) {
+      const uint32_t bit = (uint32_t)(path >> (s - 1 - i)) & 1u;  // block-uniform
+      const Cw cw = LoadCw(a.cw_seed, a.ccl, a.ccr, cw0 + i);
+      WalkStep(x, t, bit, cw, DpfSelect{{}, bit != 0}, L);
+    }
+#pragma unroll 1
+    for (int i = 0; i < 6; ++i) {
+      const uint32_t bit = ((uint32_t)lane >> (5 - i)) & 1u;
+      const Cw cw = LoadCw(a.cw_seed, a.ccl, a.ccr, cw0 + s + i);
+      WalkStep(x, t, bit, cw, DpfMasked<1>{{0u - bit}}, L);
+    }
+    nodes[lane] = make_uint4(x[0] | t, x[1], x[2], x[3]);
+  }
+  __syncthreads();
+  // 2. breadth-first: level j has 128 << j children, child c of parent c / 2
+  uint32_t x[4] = {0u, 0u, 0u, 0u}, t = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool active = wave < (2 << j);  // wave-uniform
+    if (active) {
+      const uint4 p = nodes[tid >> 1];
+      x[0] = p.x & ~1u;
+      x[1] = p.y;
+      x[2] = p.z;
+      x[3] = p.w;
+      t = p.x & 1u;
+      const uint32_t bit = (uint32_t)tid & 1u;
+      const Cw cw = LoadCw(a.cw_seed, a.ccl, a.ccr, cw0 + s + 6 + j);
+      WalkStep(x, t, bit, cw, DpfMasked<1>{{0u - bit}}, L);
+    }
+    if (j < 3) {
+      __syncthreads();  // every parent of this level has been read
+      if (active) nodes[tid] = make_uint4(x[0] | t, x[1], x[2], x[3]);
+      __syncthreads();
+    }
+  }
+  // 3. leaves: hash, convert, correct, store
+  ExpandArgs ak = a;
+  if constexpr (kBatched) ak.out += key * a.key_out_stride;
+  ExpandCtx Ec{ak, vt, L};
+  if constexpr (kBatched) {
+    const uint4 c = a.key_corr[key];
+    Ec.per_key = true;
+    Ec.kcorr[0] = c.x;
+    Ec.kcorr[1] = c.y;
+    Ec.kcorr[2] = c.z;
+    Ec.kcorr[3] = c.w;
+    Ec.kparty = a.key_party[key];
+  }
+  const int64_t g0 = chunk << K;  // first tree leaf of the block (per key if batched)
+  if constexpr (E == 0) {
+    uint32_t xs[1][4] = {{x[0], x[1], x[2], x[3]}};
+    uint32_t h[1][BN][4];
+    HashWords<1, BN, true>(xs, h, L);
+    Em::Emit(Ec, h[0], t, g0 + tid);
+  } else {
+    const Cw cw = LoadCw(a.cw_seed, a.ccl, a.ccr, cw0 + s + 10);
+    uint32_t l[4], r[4], tl, tr;
+    Expand2(x, t, cw, L, l, tl, r, tr);
+    if constexpr (BN == 1) {
+      uint32_t xs[2][4] = {{l[0], l[1], l[2], l[3]}, {r[0], r[1], r[2], r[3]}};
+      uint32_t h[2][1][4];
+      HashWords<2, 1, true>(xs, h, L);
+      Em::Emit(Ec, h[0], tl, g0 + 2 * tid);
+      Em::Emit(Ec, h[1], tr, g0 + 2 * tid + 1);
+    } else {
+      uint32_t xl[1][4] = {{l[0], l[1], l[2], l[3]}};
+      uint32_t h[1][BN][4];
+      HashWords<1, BN, true>(xl, h, L);
+      Em::Emit(Ec, h[0], tl, g0 + 2 * tid);
+      uint32_t xr[1][4] = {{r[0], r[1], r[2], r[3]}};
+      HashWords<1, BN, true>(xr, h, L);
+      Em::Emit(Ec, h[0], tr, g0 + 2 * tid + 1);
+    }
+  }
+}
+
+template <int E, class Em>
+int LaunchExpandCoop(hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
+  const int64_t cpk = a.chunk_end - a.chunk_begin;
+  int64_t blocks = cpk;
+  if (a.batched) {
+    if constexpr (!Em::kCanBatch) {
+      return SetError(DPF_AMD_INTERNAL, "batched expansion needs a directly convertible type");
+    } else {
+      blocks = cpk * a.num_keys;
+      if (blocks < 1 || blocks > INT32_MAX)
+        return SetError(DPF_AMD_INVALID_ARGUMENT, "batched expansion grid out of range");
+      hipLaunchKernelGGL((KExpandCoop<E, Em, true>), dim3((unsigned)blocks), dim3(kCoopBlock), 0,
+                         st, a, vt);
+      return LaunchCheck("expand kernel launch");
+    }
+  }
+  if (blocks < 1 || blocks > INT32_MAX)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "expansion grid out of range");
+  hipLaunchKernelGGL((KExpandCoop<E, Em, false>), dim3((unsigned)blocks), dim3(kCoopBlock), 0, st,
+                     a, vt);
+  return LaunchCheck("expand kernel launch");
+}
+
+// D >= 0: KExpand with DFS depth D; D = -1 / -2: KExpandCoop with E = 0 / 1.
 template <class Em>
 int LaunchExpandAnyD(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
+  if (D == -1) return LaunchExpandCoop<0, Em>(st, a, vt);
+  if (D == -2) return LaunchExpandCoop<1, Em>(st, a, vt);
   switch (D) {
     case 0:
       return LaunchExpand<0, Em>(grid, st, a, vt);

@@ -54,6 +54,22 @@ int CopyFromMappedHost(void* dst, const void* mapped_src, size_t bytes, void* st
 int MakeVtDev(const dpf_amd_value_type& vt, const uint64_t* correction,
               int party, int cepb, VtDev* out);
 
+// Full-domain expansion of leaves [leaf_begin, leaf_end) of each of
+// num_keys keys of one single-scalar directly convertible type in one
+// launch (KExpandCoop, batched): root_seeds / root_cb [key], correction
+// words [key][level], key_corr [key] (PackedCorrection), key_party [key];
+// key k's outputs at out + k * (leaf_end - leaf_begin) * cepb * out_stride.
+// Needs num_levels >= 11.  Device pointers, stream-ordered.
+int ExpandBatched(int64_t num_keys, const void* root_seeds, const uint8_t* root_cb,
+                  int num_levels, const void* correction_seeds, const uint8_t* ccl,
+                  const uint8_t* ccr, const dpf_amd_value_type* vt, const void* key_corr,
+                  const int8_t* key_party, int cepb, int64_t leaf_begin, int64_t leaf_end,
+                  void* out, void* stream);
+// The value correction of a single-scalar direct type packed like one hashed
+// block (the form KExpand's EmitDirect adds), for ExpandBatched's key_corr.
+int PackedCorrection(const dpf_amd_value_type& vt, const uint64_t* correction, int cepb,
+                     uint64_t out[2]);
+
 // dpf_amd_evaluate_points_batched with implicit paths over the tree-index
 // range [first_point, first_point + points_per_key) of every key (the leaf
 // range of a batched selection expansion on one shard of a database).

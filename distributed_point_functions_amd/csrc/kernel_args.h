@@ -45,6 +45,17 @@ struct ExpandArgs {
   int64_t leaf_end;
   int32_t walk;  // levels walked per thread before the DFS
   int32_t pad;
+  // Batched keys (KExpandCoop<.., true>): key k = blockIdx.x / (chunk_end -
+  // chunk_begin) has root_seeds[k] / root_cb[k], correction words
+  // [k * num_levels + level], value correction key_corr[k] (packed block of
+  // a single-scalar direct type) and party key_party[k]; the leaf range is
+  // per key and key k's outputs start at out + k * key_out_stride bytes.
+  int32_t batched;
+  int32_t num_levels;
+  int64_t num_keys;
+  int64_t key_out_stride;
+  const uint4* key_corr;
+  const int8_t* key_party;
 };
 
 struct WalkArgs {

@@ -36,6 +36,16 @@ int GridFor(int64_t items, int block, int max_blocks) {
   return (int)g;
 }
 
+// KExpandCoop variant for a launch of `leaves` tree leaves: 2048 leaves per
+// block (E = 1, -2) once that still gives >= 512 blocks (two per CU),
+// otherwise 1024 (E = 0, -1).
+int CoopDepth(int64_t leaves) { return leaves >= (int64_t{1} << 20) ? -2 : -1; }
+
+bool SingleDirect(const VtDev& vt) {
+  return vt.direct && vt.ns == 1 && vt.sc[0].in_off == 0 && vt.sc[0].out_off == 0 &&
+         vt.stride == vt.sc[0].bytes && vt.bn == 1 && vt.epb * vt.sc[0].bytes == 16;
+}
+
 KeyPair MakeKeyPair(uint64_t l_lo, uint64_t l_hi, uint64_t r_lo, uint64_t r_hi) {
   KeyPair kp;
   kp.k[0] = ExpandAesKey(l_lo, l_hi);
@@ -52,10 +62,7 @@ int BnTemplate(int bn) {
 // Picks the emitter for the value type.
 int LaunchExpandForType(int D, int grid, hipStream_t st, const ExpandArgs& a,
                         const VtDev& vt) {
-  const bool single_direct = vt.direct && vt.ns == 1 && vt.sc[0].in_off == 0 &&
-                             vt.sc[0].out_off == 0 && vt.stride == vt.sc[0].bytes &&
-                             vt.bn == 1 && vt.epb * vt.sc[0].bytes == 16;
-  if (single_direct) {
+  if (SingleDirect(vt)) {
     switch (vt.sc[0].bytes) {
       case 1:
         return LaunchExpandDirect1(D, grid, st, a, vt);
@@ -253,28 +260,38 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
   const int64_t range = leaf_end - leaf_begin;
   if (D == 8 && (range >> 8) < (int64_t{1} << 17)) D = 4;
   if (D == 4 && (range >> 4) < (int64_t{1} << 16)) D = 2;
+  // Below 2^25 tree leaves the cooperative kernel computes every tree node
+  // once per block instead of one root walk per thread (KExpandCoop,
+  // expand_device.h): D = -1 (1024 leaves per block) or -2 (2048).
+  if (num_levels >= 11 && range < (int64_t{1} << 25)) D = CoopDepth(range);
   const int forced = t_expand_depth;
   if (forced > 0 && forced <= num_levels) D = forced;
-  ExpandArgs a;
+  if (forced < 0 && num_levels >= 10 - forced - 1) D = forced;
+  ExpandArgs a{};
   a.root_seeds = (const uint4*)root_seeds;
   a.root_cb = root_control_bits;
   a.cw_seed = (const uint4*)correction_seeds;
   a.ccl = ccl;
   a.ccr = ccr;
   a.out = (char*)out;
-  a.walk = num_levels - D;
+  const int sub = D >= 0 ? D : 9 - D;  // log2 leaves per thread (KExpand) or per block (coop)
+  a.walk = num_levels - sub;
   a.pad = 0;
-  a.chunk_begin = leaf_begin >> D;
-  a.chunk_end = (leaf_end + (1ll << D) - 1) >> D;
+  a.chunk_begin = leaf_begin >> sub;
+  a.chunk_end = (leaf_end + (1ll << sub) - 1) >> sub;
   a.leaf_begin = leaf_begin;
   a.leaf_end = leaf_end;
+  a.num_levels = num_levels;
+  a.num_keys = 1;
   // LaunchExpand caps the grid (DPF_EXPAND_MAX_GRID).
   const int grid = GridFor(a.chunk_end - a.chunk_begin, kExpandBlock, INT32_MAX);
   return LaunchExpandForType(D, grid, (hipStream_t)stream, a, dev);
 }
 
 int dpf_amd_set_expand_depth(int depth) {
-  if (depth != 0 && depth != 1 && depth != 2 && depth != 4 && depth != 8) return -1;
+  if (depth != 0 && depth != 1 && depth != 2 && depth != 4 && depth != 8 && depth != -1 &&
+      depth != -2)
+    return -3;
   const int old = t_expand_depth;
   t_expand_depth = depth;
   return old;
@@ -368,6 +385,54 @@ int dpf_amd_evaluate_points_batched(int64_t num_keys, int64_t points_per_key,
 }  // extern "C"
 
 namespace dpf_amd {
+int ExpandBatched(int64_t num_keys, const void* root_seeds, const uint8_t* root_cb,
+                  int num_levels, const void* correction_seeds, const uint8_t* ccl,
+                  const uint8_t* ccr, const dpf_amd_value_type* vt, const void* key_corr,
+                  const int8_t* key_party, int cepb, int64_t leaf_begin, int64_t leaf_end,
+                  void* out, void* stream) {
+  if (num_keys <= 0 || leaf_end <= leaf_begin) return DPF_AMD_OK;
+  if (!vt || num_levels < 11 || num_levels > 62 || leaf_begin < 0 ||
+      leaf_end > (int64_t{1} << num_levels))
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "bad batched expansion");
+  VtDev dev;
+  int rc = MakeVtDev(*vt, nullptr, 0, cepb, &dev);
+  if (rc != DPF_AMD_OK) return rc;
+  if (!SingleDirect(dev))
+    return SetError(DPF_AMD_UNIMPLEMENTED, "batched expansion needs a directly convertible type");
+  const int64_t range = leaf_end - leaf_begin;
+  const int D = (range >= 2048 && num_keys * range >= (int64_t{1} << 20)) ? -2 : -1;
+  const int sub = 9 - D;
+  ExpandArgs a{};
+  a.root_seeds = (const uint4*)root_seeds;
+  a.root_cb = root_cb;
+  a.cw_seed = (const uint4*)correction_seeds;
+  a.ccl = ccl;
+  a.ccr = ccr;
+  a.out = (char*)out;
+  a.walk = num_levels - sub;
+  a.chunk_begin = leaf_begin >> sub;
+  a.chunk_end = (leaf_end + (1ll << sub) - 1) >> sub;
+  a.leaf_begin = leaf_begin;
+  a.leaf_end = leaf_end;
+  a.batched = 1;
+  a.num_levels = num_levels;
+  a.num_keys = num_keys;
+  a.key_out_stride = range * cepb * dev.stride;  // single direct: stride = element bytes
+  a.key_corr = (const uint4*)key_corr;
+  a.key_party = key_party;
+  return LaunchExpandForType(D, 1, (hipStream_t)stream, a, dev);
+}
+
+int PackedCorrection(const dpf_amd_value_type& vt, const uint64_t* correction, int cepb,
+                     uint64_t out[2]) {
+  VtDev dev;
+  const int rc = MakeVtDev(vt, correction, 0, cepb, &dev);
+  if (rc != DPF_AMD_OK) return rc;
+  out[0] = (uint64_t)dev.corr_packed;
+  out[1] = (uint64_t)(dev.corr_packed >> 64);
+  return DPF_AMD_OK;
+}
+
 int EvaluatePointsBatchedRange(int64_t num_keys, int64_t first_point, int64_t points_per_key,
                                const void* key_seeds, const uint8_t* key_control_bits,
                                int num_levels, const void* correction_seeds, const uint8_t* ccl,

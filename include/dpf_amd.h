@@ -136,11 +136,13 @@ int dpf_amd_expand_and_correct(
     int corrected_elements_per_block, int64_t leaf_begin, int64_t leaf_end,
     void* out, void* stream);
 
-/* Testing knob (calling thread only): forces the register-DFS depth D of the fused
- * expansion kernel to 1, 2, 4 or 8 whenever num_levels >= D, so the deep
- * kernels that large launches select can be checked on small domains.
- * 0 restores the automatic choice.  Returns the previous setting, or -1 for
- * an invalid depth (setting unchanged). */
+/* Testing knob (calling thread only): forces the register-DFS depth D of the
+ * fused expansion kernel KExpand to 1, 2, 4 or 8 whenever num_levels >= D,
+ * or the cooperative kernel KExpandCoop with 1024 (-1) or 2048 (-2) leaves
+ * per block whenever num_levels >= 10 / 11, so the kernels that other launch
+ * sizes select can be checked on small domains.  0 restores the automatic
+ * choice.  Returns the previous setting, or -3 for an invalid value
+ * (setting unchanged). */
 int dpf_amd_set_expand_depth(int depth);
 
 /* Testing knob (calling thread only): which XOR scan dpf_amd_inner_product

@@ -1,13 +1,17 @@
 """Parity of the expansion kernels that the production launches select, and
 of the benchmarked configuration at its full size.
 
-`dpf_amd_expand_and_correct` picks the register-DFS depth D of KExpand<D>
-from the launch size (kernels_capi.cc): D = 8 once a launch covers >= 2^25
-tree leaves, D = 4 from 2^20.  These tests
-  * force D in {1, 2, 4, 8} (dpf_amd_set_expand_depth) on small domains and
-    compare every output of every value type with the oracle;
-  * run the automatic choice at sizes where it picks D = 4 (2^20 and 2^24
-    tree leaves) and D = 8 (2^25) and compare every output with the oracle;
+`dpf_amd_expand_and_correct` picks the kernel from the launch size
+(kernels_capi.cc): KExpand<8> (register DFS of depth 8 per thread) once a
+launch covers >= 2^25 tree leaves, the cooperative KExpandCoop (2^10 or 2^11
+leaves per block) below that when the tree has >= 11 levels, KExpand<D> with
+D = 4 / 2 / 1 on smaller trees.  These tests
+  * force D in {1, 2, 4, 8} and each KExpandCoop variant
+    (dpf_amd_set_expand_depth) on small domains and compare every output of
+    every value type with the oracle;
+  * run the automatic choice at sizes where it picks KExpandCoop (2^11-2^24
+    tree leaves) and KExpand<8> (2^25) and compare every output with the
+    oracle;
   * run the c5 bench configuration itself (log_domain_size 32,
     Tuple<uint32, IntModN<uint64, 2^64-59>>, the KExpand<8, EmitU32ModN64>
     launch the bench times) for both parties: the share sum over all 2^32
@@ -115,6 +119,50 @@ def test_forced_depth_leaf_ranges(K, cuda, depth):
             _assert_host_layout_equals_words(C5, got, want[lo:hi], "[%d, %d)" % (lo, hi))
 
 
+@pytest.mark.parametrize("coop", [-1, -2])
+@pytest.mark.parametrize("spec", TYPES, ids=[repr(t) for t in TYPES])
+def test_cooperative_kernel_matches_oracle(K, cuda, spec, coop):
+    """KExpandCoop (1024 / 2048 leaves per block: wave-0 walk to 64
+    sub-roots, four LDS breadth-first levels, one leaf per thread) forced on
+    a 2^16-element domain of every value type, both parties."""
+    d, k0, k1, alpha, beta = _keys(spec, 16, seed=20 - coop)
+    assert d.hierarchy_to_tree(0) >= 11
+    with K.forced_expand_depth(coop):
+        for key in (k0, k1):
+            want = d.evaluate_until_words(0, [], d.create_evaluation_context(key))
+            got = _expand(K, cuda, d, key, spec).cpu().numpy()
+            _assert_host_layout_equals_words(spec, got, want, "party %d" % key.party)
+
+
+@pytest.mark.parametrize("coop", [-1, -2])
+def test_cooperative_kernel_leaf_ranges(K, cuda, coop):
+    """Ragged leaf ranges inside and across the 2^10 / 2^11-leaf blocks."""
+    d, k0, _, _, _ = _keys(C5, 15, seed=4)
+    want = d.evaluate_until_words(0, [], d.create_evaluation_context(k0))
+    n = 1 << d.hierarchy_to_tree(0)
+    with K.forced_expand_depth(coop):
+        for lo, hi in [(0, n), (1, n - 1), (1023, 1025), (2047, 2049), (3000, 3001),
+                       (4097, 20000), (n - 300, n)]:
+            got = _expand(K, cuda, d, k0, C5, lo, hi).cpu().numpy()
+            _assert_host_layout_equals_words(C5, got, want[lo:hi], "[%d, %d)" % (lo, hi))
+
+
+@pytest.mark.parametrize("ld", [12, 20, 21, 25])
+def test_automatic_cooperative_launch_matches_oracle(K, cuda, ld):
+    """Sizes where the automatic choice runs KExpandCoop: uint64 at
+    log_domain_size 12 (2^11 tree leaves, two blocks) and 20 (c1: 2^19 tree
+    leaves) -> 1024-leaf blocks; 21 and 25 (2^20, 2^24 tree leaves) ->
+    2048-leaf blocks; every output against the oracle."""
+    import torch
+    spec = ("int", 64)
+    d, k0, k1, alpha, beta = _keys(spec, ld, seed=19)
+    for key in (k0, k1):
+        want = d.evaluate_until_words(0, [], d.create_evaluation_context(key))
+        got = _expand(K, cuda, d, key, spec).cpu().numpy()
+        _assert_host_layout_equals_words(spec, got, want, "ld %d party %d" % (ld, key.party))
+    torch.cuda.empty_cache()
+
+
 def test_forced_depth_knob_validates():
     from distributed_point_functions_amd import kernels as K
     with pytest.raises(ValueError):
@@ -126,7 +174,7 @@ def test_forced_depth_knob_validates():
 # The automatic choice at the sizes where it selects D = 4 and D = 8
 # ---------------------------------------------------------------------------
 
-AUTO = [  # (spec, log_domain) -> tree levels L; D = 4 at L = 20 / 24, D = 8 at L = 25
+AUTO = [  # (spec, log_domain) -> tree levels L; KExpandCoop at L = 20 / 24, KExpand<8> at L = 25
     (C5, 20), (C5, 25),
     (("int", 64), 21), (("int", 64), 25), (("int", 64), 26),
     (("xor", 128), 20), (("xor", 128), 25),
