@@ -95,6 +95,8 @@ def lib():
          U64, U64, U64, U64, P, P, P)
     _sig(L, "dpf_amd_expand_and_correct", I32, I64, P, P, I32, P, P, P,
          ctypes.POINTER(ValueTypeDesc), P, I32, I32, I64, I64, P, P)
+    _sig(L, "dpf_amd_expand_and_correct_batched", I32, I64, P, P, I32, P, P, P,
+         ctypes.POINTER(ValueTypeDesc), P, P, I32, I64, I64, P, P)
     _sig(L, "dpf_amd_evaluate_points", I32, I64, P, P, P, I32, I32, I64, P, P, P,
          ctypes.POINTER(ValueTypeDesc), P, P, I32, P, P, P, P, P, P)
     _sig(L, "dpf_amd_dcf_evaluate", I32, I64, P, P, P, P, I32, P, P, P, P,

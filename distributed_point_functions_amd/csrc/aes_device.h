@@ -544,6 +544,7 @@ struct ExpandCtx {
   bool per_key = false;
   uint32_t kcorr[4] = {0u, 0u, 0u, 0u};
   int kparty = 0;
+  int64_t cw0 = 0;  // first correction word of this key ([key][level] layout)
 };
 
 // Value PRG of one seed: block j = H_value(seed + j) (cc:523-547).

@@ -285,7 +285,7 @@ __device__ __forceinline__ void Dfs(const ExpandCtx& E, LeafStage& S, const uint
     HashWords<1, BN, (D > 0)>(xs, h, E.L);
     EmitStagedLeaf<D, Em, BN>(E, S, h[0], t, chunk, j);
   } else {
-    const Cw cw = LoadCw(E.a.cw_seed, E.a.ccl, E.a.ccr, level);
+    const Cw cw = LoadCw(E.a.cw_seed, E.a.ccl, E.a.ccr, E.cw0 + level);
     uint32_t l[4], r[4], tl, tr;
     Expand2(x, t, cw, E.L, l, tl, r, tr);
     if constexpr (DEPTH == 1 && BN == 1) {
@@ -313,29 +313,35 @@ __device__ __forceinline__ void Dfs(const ExpandCtx& E, LeafStage& S, const uint
   }
 }
 
-template <int D, class Em>
+// Batched keys (kBatched, ExpandArgs::batched): lane i's chunk id maps to
+// key id / (chunk_end - chunk_begin) with that key's root, correction words,
+// value correction and party; leaf ranges and outputs are per key.
+template <int D, class Em, bool kBatched = false>
 __global__ __launch_bounds__(kBlockOf<Em>, kWavesOf<Em>) void KExpand(ExpandArgs a, VtDev vt) {
   __shared__ uint32_t tab[kTabWords];
   FillTables(tab);
   __syncthreads();
   const Lds L = MakeLds(tab);
-  const ExpandCtx E{a, vt, L};
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t cpk = a.chunk_end - a.chunk_begin;
+  const int64_t total = kBatched ? cpk * a.num_keys : cpk;
   // Every lane runs the same number of iterations (uniform trip count), so
   // the per-level wave votes below see all lanes; lanes past the end idle.
-  const int64_t first = a.chunk_begin + (int64_t)blockIdx.x * blockDim.x;
-  for (int64_t base = first; base < a.chunk_end; base += stride) {
-    const int64_t chunk = base + threadIdx.x;
-    const bool live = chunk < a.chunk_end;
-    const int64_t c = live ? chunk : a.chunk_end - 1;
-    const int64_t root = c >> a.walk;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < total; base += stride) {
+    const int64_t id = base + threadIdx.x;
+    const bool live = id < total;
+    const int64_t cid = live ? id : total - 1;
+    const int64_t key = kBatched ? cid / cpk : 0;
+    const int64_t c = a.chunk_begin + (kBatched ? cid - key * cpk : cid);
+    const int64_t root = kBatched ? key : c >> a.walk;
+    const int64_t cw0 = kBatched ? key * a.num_levels : 0;
     const uint64_t path = (uint64_t)c & ((a.walk >= 63) ? ~0ull : ((1ull << a.walk) - 1));
     uint4 s = a.root_seeds[root];
     uint32_t x[4] = {s.x, s.y, s.z, s.w};
     uint32_t t = a.root_cb[root];
     for (int i = 0; i < a.walk; ++i) {
       const uint32_t bit = (uint32_t)(path >> (a.walk - 1 - i)) & 1u;
-      const Cw cw = LoadCw(a.cw_seed, a.ccl, a.ccr, i);
+      const Cw cw = LoadCw(a.cw_seed, a.ccl, a.ccr, cw0 + i);
       // The upper path bits are shared by the whole wave: one AES with the
       // key picked by a scalar select.  Lanes that disagree compute both
       // children with the uniform keys and keep the path child.
@@ -354,6 +360,19 @@ __global__ __launch_bounds__(kBlockOf<Em>, kWavesOf<Em>) void KExpand(ExpandArgs
         t = bit ? tr : tl;
       }
     }
+    ExpandArgs ak = a;
+    ExpandCtx E{ak, vt, L};
+    if constexpr (kBatched) {
+      ak.out += key * a.key_out_stride;
+      const uint4 kc = a.key_corr[key];
+      E.per_key = true;
+      E.kcorr[0] = kc.x;
+      E.kcorr[1] = kc.y;
+      E.kcorr[2] = kc.z;
+      E.kcorr[3] = kc.w;
+      E.kparty = a.key_party[key];
+      E.cw0 = cw0;
+    }
     LeafStage S;
     if (live) Dfs<D, D, Em>(E, S, x, t, a.walk, c, 0);
   }
@@ -366,10 +385,18 @@ int LaunchExpand(int, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
   // back-fills.  c5: 2^24 subtrees / 768 = 21845 blocks -> 166.8 ms, vs
   // 173.8 ms capped at 2730 blocks and 180.5 ms at one resident round.
   constexpr int block = kBlockOf<Em>;
-  const int64_t chunks = a.chunk_end - a.chunk_begin;
+  const int64_t chunks = (a.chunk_end - a.chunk_begin) * (a.batched ? a.num_keys : 1);
   const int grid = (int)std::max<int64_t>(
       1, std::min<int64_t>((chunks + block - 1) / block, DPF_EXPAND_MAX_GRID));
-  hipLaunchKernelGGL((KExpand<D, Em>), dim3(grid), dim3(block), 0, st, a, vt);
+  if (a.batched) {
+    if constexpr (Em::kCanBatch) {
+      hipLaunchKernelGGL((KExpand<D, Em, true>), dim3(grid), dim3(block), 0, st, a, vt);
+    } else {
+      return SetError(DPF_AMD_INTERNAL, "batched expansion needs a directly convertible type");
+    }
+  } else {
+    hipLaunchKernelGGL((KExpand<D, Em, false>), dim3(grid), dim3(block), 0, st, a, vt);
+  }
   return LaunchCheck("expand kernel launch");
 }
 

@@ -9,11 +9,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "aes_tables.h"
 #include "dpf_amd.h"
 #include "internal.h"
 #include "kernel_args.h"
+#include "host_device.h"
 
 namespace dpf_amd {
 
@@ -36,10 +38,25 @@ int GridFor(int64_t items, int block, int max_blocks) {
   return (int)g;
 }
 
-// KExpandCoop variant for a launch of `leaves` tree leaves: 2048 leaves per
-// block (E = 1, -2) once that still gives >= 512 blocks (two per CU),
-// otherwise 1024 (E = 0, -1).
-int CoopDepth(int64_t leaves) { return leaves >= (int64_t{1} << 20) ? -2 : -1; }
+// Kernel for a single-key launch of `leaves` tree leaves of a tree of >= 11
+// levels, from tools/expand_sweep.py on MI355X (profiles/sweep_*_r03e.log):
+// below 2^20 leaves the launch is latency-bound (a 2^11-leaf, one-block
+// launch takes 27 us; 2^19 leaves: KExpandCoop 53-55 us, KExpand<2> 59,
+// KExpand<4> 112), and KExpandCoop computes each tree node once; from 2^20
+// on, KExpand<4>'s full-occupancy register DFS wins (2^21: 0.127 vs 0.143
+// ms; 2^23: 0.357 vs 0.549) until KExpand<8> at 2^25.
+int CoopDepth(int64_t leaves) { return leaves >= (int64_t{1} << 19) ? -2 : -1; }
+
+// Kernel for a batched expansion of num_keys x range tree leaves
+// (tools/expand_sweep.py batched): KExpand<4> with per-lane keys from 2^22
+// leaves in total (64 keys x 2^19: 1.26 ms = 0.65 of the LDS bound; the
+// cooperative kernel 1.90, KExpand<8> 1.34), KExpandCoop with per-block
+// keys below.
+int BatchedDepth(int64_t num_keys, int64_t range) {
+  const int64_t total = num_keys * range;
+  if (total >= (int64_t{1} << 22) && range >= 16) return 4;
+  return CoopDepth(total);
+}
 
 bool SingleDirect(const VtDev& vt) {
   return vt.direct && vt.ns == 1 && vt.sc[0].in_off == 0 && vt.sc[0].out_off == 0 &&
@@ -263,7 +280,7 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
   // Below 2^25 tree leaves the cooperative kernel computes every tree node
   // once per block instead of one root walk per thread (KExpandCoop,
   // expand_device.h): D = -1 (1024 leaves per block) or -2 (2048).
-  if (num_levels >= 11 && range < (int64_t{1} << 25)) D = CoopDepth(range);
+  if (num_levels >= 11 && range < (int64_t{1} << 20)) D = CoopDepth(range);
   const int forced = t_expand_depth;
   if (forced > 0 && forced <= num_levels) D = forced;
   if (forced < 0 && num_levels >= 10 - forced - 1) D = forced;
@@ -286,6 +303,56 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
   // LaunchExpand caps the grid (DPF_EXPAND_MAX_GRID).
   const int grid = GridFor(a.chunk_end - a.chunk_begin, kExpandBlock, INT32_MAX);
   return LaunchExpandForType(D, grid, (hipStream_t)stream, a, dev);
+}
+
+int dpf_amd_expand_and_correct_batched(int64_t num_keys, const void* root_seeds,
+                                       const uint8_t* root_control_bits, int num_levels,
+                                       const void* correction_seeds, const uint8_t* ccl,
+                                       const uint8_t* ccr, const dpf_amd_value_type* vt,
+                                       const uint64_t* value_corrections, const int8_t* parties,
+                                       int corrected_elements_per_block, int64_t leaf_begin,
+                                       int64_t leaf_end, void* out, void* stream) {
+  if (num_keys < 0 || !vt || num_levels < 0 || num_levels > 62)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "bad arguments");
+  if (leaf_begin < 0 || leaf_end > (int64_t{1} << num_levels) || leaf_begin > leaf_end)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "leaf range out of bounds");
+  if (num_keys == 0 || leaf_begin == leaf_end) return DPF_AMD_OK;
+  const int per = vt->elements_per_block * vt->num_scalars;  // correction words per key
+  VtDev probe;
+  int rc = MakeVtDev(*vt, nullptr, 0, corrected_elements_per_block, &probe);
+  if (rc != DPF_AMD_OK) return rc;
+  const int64_t range = leaf_end - leaf_begin;
+  hipStream_t st = (hipStream_t)stream;
+  if (!SingleDirect(probe) || num_levels < 11 || range >= (int64_t{1} << 25)) {
+    // one launch per key (a type whose correction is not one packed block,
+    // or keys large enough to fill the GPU on their own)
+    const int64_t out_bytes = range * corrected_elements_per_block * vt->out_stride;
+    for (int64_t k = 0; k < num_keys; ++k) {
+      rc = dpf_amd_expand_and_correct(
+          1, static_cast<const char*>(root_seeds) + 16 * k, root_control_bits + k, num_levels,
+          static_cast<const char*>(correction_seeds) + 16 * k * num_levels, ccl + k * num_levels,
+          ccr + k * num_levels, vt, value_corrections + 2 * per * k, parties[k],
+          corrected_elements_per_block, leaf_begin, leaf_end,
+          static_cast<char*>(out) + k * out_bytes, stream);
+      if (rc != DPF_AMD_OK) return rc;
+    }
+    return DPF_AMD_OK;
+  }
+  std::vector<uint64_t> host(2 * num_keys + (num_keys + 15) / 16 * 2, 0);
+  for (int64_t k = 0; k < num_keys; ++k) {
+    rc = PackedCorrection(*vt, value_corrections + 2 * per * k, corrected_elements_per_block,
+                          &host[2 * k]);
+    if (rc != DPF_AMD_OK) return rc;
+  }
+  memcpy(&host[2 * num_keys], parties, num_keys);
+  namespace h = distributed_point_functions::dpf_internal_host;
+  h::DeviceBuffer dev;
+  distributed_point_functions::Status ust = dev.Upload(host.data(), 8 * host.size(), st);
+  if (!ust.ok()) return SetError(ust.raw_code(), ust.message());
+  return ExpandBatched(num_keys, root_seeds, root_control_bits, num_levels, correction_seeds, ccl,
+                       ccr, vt, dev.get(),
+                       reinterpret_cast<const int8_t*>(dev.as<char>() + 16 * num_keys),
+                       corrected_elements_per_block, leaf_begin, leaf_end, out, stream);
 }
 
 int dpf_amd_set_expand_depth(int depth) {
@@ -400,8 +467,11 @@ int ExpandBatched(int64_t num_keys, const void* root_seeds, const uint8_t* root_
   if (!SingleDirect(dev))
     return SetError(DPF_AMD_UNIMPLEMENTED, "batched expansion needs a directly convertible type");
   const int64_t range = leaf_end - leaf_begin;
-  const int D = (range >= 2048 && num_keys * range >= (int64_t{1} << 20)) ? -2 : -1;
-  const int sub = 9 - D;
+  int D = BatchedDepth(num_keys, range);
+  const int forced = t_expand_depth;
+  if (forced > 0 && forced <= num_levels) D = forced;
+  if (forced < 0) D = forced;
+  const int sub = D >= 0 ? D : 9 - D;
   ExpandArgs a{};
   a.root_seeds = (const uint4*)root_seeds;
   a.root_cb = root_cb;

@@ -97,6 +97,33 @@ def expand_and_correct(root_seeds, root_control_bits, num_levels, cw_seeds, ccl,
     return out
 
 
+def expand_and_correct_batched(root_seeds, root_control_bits, num_levels, cw_seeds, ccl, ccr,
+                               desc: "_lib.ValueTypeDesc", value_corrections, parties,
+                               corrected_elements_per_block: int, leaf_begin: int = 0,
+                               leaf_end: int = None, out: torch.Tensor = None):
+    """Leaves [leaf_begin, leaf_end) of every key in one launch (see
+    dpf_amd_expand_and_correct_batched): root_seeds (q, 2) int64, control
+    bits (q,), cw_seeds (q * num_levels, 2), ccl / ccr (q * num_levels,);
+    value_corrections: q lists of 128-bit words, parties: q ints.  Returns a
+    uint8 tensor: key k's host-layout values after key k - 1's."""
+    q = root_seeds.shape[0]
+    if leaf_end is None:
+        leaf_end = 1 << num_levels
+    count = q * (leaf_end - leaf_begin) * corrected_elements_per_block
+    if out is None:
+        out = torch.empty(count * desc.out_stride, dtype=torch.uint8, device=root_seeds.device)
+    elif out.numel() * out.element_size() < count * desc.out_stride:
+        raise ValueError("output buffer too small")
+    corr = _corr_words([w for vc in value_corrections for w in vc])
+    pa = np.ascontiguousarray(parties, dtype=np.int8)
+    check(_lib.lib().dpf_amd_expand_and_correct_batched(
+        q, dptr(root_seeds), dptr(root_control_bits), num_levels, dptr(cw_seeds), dptr(ccl),
+        dptr(ccr), ctypes.byref(desc), corr.ctypes.data_as(ctypes.c_void_p),
+        pa.ctypes.data_as(ctypes.c_void_p), corrected_elements_per_block, leaf_begin, leaf_end,
+        dptr(out), stream_ptr()))
+    return out
+
+
 class forced_expand_depth:
     """Context manager forcing the fused expansion kernel's register-DFS
     depth (dpf_amd_set_expand_depth; tests run the deep kernels that large

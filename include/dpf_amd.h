@@ -136,6 +136,24 @@ int dpf_amd_expand_and_correct(
     int corrected_elements_per_block, int64_t leaf_begin, int64_t leaf_end,
     void* out, void* stream);
 
+/* Full-domain expansion of many keys of one DPF in one launch (the selection
+ * vectors of a Q-key PIR request, or any batch of EvaluateUntil keys of a
+ * single hierarchy level): leaves [leaf_begin, leaf_end) of each key, key k's
+ * outputs at out + k * (leaf_end - leaf_begin) * corrected_elements_per_block
+ * * out_stride.  Device arrays: root_seeds [key] (128-bit), root control
+ * bits [key], correction words [key][level] (seeds 128-bit, ccl, ccr).  Host
+ * arrays: value_corrections [key][elements_per_block * num_scalars] 128-bit
+ * words, parties [key].  Single-scalar directly convertible types of >= 11
+ * tree levels run one KExpand / KExpandCoop grid over all keys; other types
+ * one launch per key.  Stream-ordered on `stream`. */
+int dpf_amd_expand_and_correct_batched(
+    int64_t num_keys, const void* root_seeds, const uint8_t* root_control_bits,
+    int num_levels, const void* correction_seeds, const uint8_t* ccl,
+    const uint8_t* ccr, const dpf_amd_value_type* vt,
+    const uint64_t* value_corrections, const int8_t* parties,
+    int corrected_elements_per_block, int64_t leaf_begin, int64_t leaf_end,
+    void* out, void* stream);
+
 /* Testing knob (calling thread only): forces the register-DFS depth D of the
  * fused expansion kernel KExpand to 1, 2, 4 or 8 whenever num_levels >= D,
  * or the cooperative kernel KExpandCoop with 1024 (-1) or 2048 (-2) leaves

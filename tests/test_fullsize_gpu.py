@@ -371,3 +371,37 @@ def test_c5_eight_rank_split_reproduces_one_rank(K, cuda, c5_full):
             lo, hi = sharding.block_range(n, world, rank)
             _expand(K, cuda, d, key, C5, lo, hi, out=buf[lo * 16:hi * 16])
         assert _chunked_equal(buf, full), world
+
+
+@pytest.mark.parametrize("variant", [0, 2, 4, 8, -1, -2])
+@pytest.mark.parametrize("spec,ld", [(("xor", 128), 14), (("int", 64), 15), (("int", 32), 16),
+                                     (("int", 8), 18), (C5, 13)])
+def test_batched_keys_match_oracle(K, cuda, spec, ld, variant):
+    """dpf_amd_expand_and_correct_batched: several keys (both parties mixed,
+    different alphas / betas) in one grid — KExpand with per-lane keys or
+    KExpandCoop with per-block keys — on a ragged leaf range, every output
+    against the oracle (C5 takes the per-key path)."""
+    from distributed_point_functions_amd import value_types as vtm
+    import torch
+    ks = [_keys(spec, ld, seed=100 + i) for i in range(5)]
+    keys = [(d, k0 if i % 2 else k1) for i, (d, k0, k1, _, _) in enumerate(ks)]
+    d0 = keys[0][0]
+    L = d0.hierarchy_to_tree(0)
+    if variant > L or (variant < 0 and L < 10 - variant - 1):
+        pytest.skip("variant needs more tree levels")
+    n = 1 << L
+    lo, hi = (3, n - 5) if n > 64 else (0, n)
+    cepb = 1 << (ld - L)
+    arrs = [_key_arrays(K, cuda, d, k) for d, k in keys]
+    vt = vtm.from_spec(spec)
+    with K.forced_expand_depth(variant):
+        got = K.expand_and_correct_batched(
+            torch.cat([a["seed"] for a in arrs]), torch.cat([a["cb"] for a in arrs]), L,
+            torch.cat([a["cw"] for a in arrs]), torch.cat([a["ccl"] for a in arrs]),
+            torch.cat([a["ccr"] for a in arrs]), vt.descriptor(d0.blocks_needed(0)),
+            [a["corr"] for a in arrs], [a["party"] for a in arrs], cepb, lo, hi).cpu().numpy()
+    per = (hi - lo) * cepb * vt.descriptor(d0.blocks_needed(0)).out_stride
+    for i, (d, k) in enumerate(keys):
+        want = d.evaluate_until_words(0, [], d.create_evaluation_context(k))
+        _assert_host_layout_equals_words(spec, got[i * per:(i + 1) * per],
+                                         want[lo * cepb:hi * cepb], "key %d" % i)

@@ -458,12 +458,28 @@ def cpp(dev, reps):
     import subprocess
     from distributed_point_functions_amd import build_native
     torch.cuda.synchronize()
-    res = subprocess.run([build_native.CPP_BENCH, str(reps)], capture_output=True, text=True,
-                         timeout=600)
+    res = subprocess.run([build_native.CPP_BENCH, str(reps), "c1,c2,c2a,c3"], capture_output=True,
+                         text=True, timeout=600)
     if res.returncode != 0:
         raise RuntimeError("cpp_api_bench failed: " + res.stderr[-2000:])
     lines = [json.loads(x) for x in res.stdout.splitlines() if x.startswith("{")]
-    return {"config": "cpp", "workload": "C++ API c1-c3", "results": lines}
+    return {"config": "cpp", "workload": "C++ API c1, c2 (EvaluateAt, EvaluateAndApply), c3",
+            "results": lines}
+
+
+def cpp4(dev, reps):
+    """c4 through the C++ API: DenseDpfPirServer::HandleRequest over 2^26 x
+    256 B records at Q = 1, 8, 64 (tools/cpp_api_bench.cc)."""
+    import subprocess
+    from distributed_point_functions_amd import build_native
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    res = subprocess.run([build_native.CPP_BENCH, str(reps), "c4"], capture_output=True,
+                         text=True, timeout=900)
+    if res.returncode != 0:
+        raise RuntimeError("cpp_api_bench c4 failed: " + res.stderr[-2000:])
+    lines = [json.loads(x) for x in res.stdout.splitlines() if x.startswith("{")]
+    return {"config": "cpp4", "workload": "C++ API c4 HandleRequest", "results": lines}
 
 
 def main():

@@ -6,12 +6,19 @@
 //   c1  EvaluateNext<uint64_t> full domain, log_domain_size 20
 //   c2  EvaluateAt<uint128> of 16384 random points for each of 64 keys,
 //       log_domain_size 128 (2^20 points)
+//   c2a the same 2^20 (key, point) pairs through EvaluateAndApply<uint128>
+//       (h:1072-1198, 64 distinct keys each repeated for its 16384 points)
 //   c3  16 hierarchy levels of 8 bits, uint64, EvaluateNext on 2^16 distinct
 //       surviving prefixes per level (distributed_point_function_benchmark.cc:
 //       154-191 shape)
+//   c4  (only when asked: 16 GiB of host records) DenseDpfPirServer::
+//       HandleRequest over 2^26 records x 256 B for Q = 1, 8, 64 keys per
+//       request (pir/dense_dpf_pir_database_benchmark.cc:37-157 batch shapes;
+//       pir/dense_dpf_pir_server.cc:92-127), both parties, reconstruction
+//       checked
 //
 // Built by distributed_point_functions_amd/build_native.py next to the
-// library; run on the GPU box: _native/cpp_api_bench [reps].
+// library; run on the GPU box: _native/cpp_api_bench [reps] [c1,c2,c2a,c3,c4].
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -20,6 +27,10 @@
 #include <set>
 #include <vector>
 
+#include <cstring>
+#include <string>
+
+#include "dpf_amd/dense_dpf_pir_server.h"
 #include "dpf_amd/distributed_point_function.h"
 
 using namespace distributed_point_functions;
@@ -112,6 +123,137 @@ void C2(int reps) {
   std::printf("{\"config\": \"c2\", \"api\": \"C++ EvaluateAt<uint128>, 64 keys x 16384 points\", "
               "\"points\": %d, \"best_ms\": %.3f, \"points_per_s\": %.4g, \"correct\": %s}\n",
               nkeys * per, 1e3 * best, nkeys * per / best, ok ? "true" : "false");
+}
+
+void C2Apply(int reps) {
+  DpfParameters p;
+  p.set_log_domain_size(128);
+  p.mutable_value_type()->mutable_integer()->set_bitsize(128);
+  auto dpf = DistributedPointFunction::Create(p);
+  OK_OR_DIE(dpf);
+  std::mt19937_64 rng(2);
+  const int nkeys = 64, per = 1 << 14;
+  std::vector<DpfKey> k0s, k1s;
+  std::vector<uint128> betas, alphas;
+  for (int k = 0; k < nkeys; ++k) {
+    const uint128 alpha = MakeUint128(rng(), rng()), beta = MakeUint128(rng(), rng());
+    auto keys = (*dpf)->GenerateKeys(alpha, beta);
+    OK_OR_DIE(keys);
+    k0s.push_back(keys->first);
+    k1s.push_back(keys->second);
+    betas.push_back(beta);
+    alphas.push_back(alpha);
+  }
+  // key i / per at point i: each key's first point is its alpha
+  std::vector<const DpfKey*> kp0(nkeys * per), kp1(nkeys * per);
+  std::vector<uint128> pts(nkeys * per);
+  for (int i = 0; i < nkeys * per; ++i) {
+    kp0[i] = &k0s[i / per];
+    kp1[i] = &k1s[i / per];
+    pts[i] = (i % per == 0) ? alphas[i / per] : MakeUint128(rng(), rng());
+  }
+  std::vector<uint128> a(pts.size()), b(pts.size());
+  double best = 1e30;
+  for (int r = 0; r <= reps; ++r) {
+    const double t0 = Now();
+    Status st = (*dpf)->EvaluateAndApply<uint128>(
+        Span<const DpfKey* const>(kp0.data(), kp0.size()), pts, [&](Span<const uint128> v) {
+          std::memcpy(a.data(), v.data(), 16 * v.size());
+          return true;
+        });
+    const double t = Now() - t0;
+    if (!st.ok()) {
+      std::fprintf(stderr, "EvaluateAndApply: %s\n", st.ToString().c_str());
+      std::exit(1);
+    }
+    if (r > 0) best = std::min(best, t);
+  }
+  Status st = (*dpf)->EvaluateAndApply<uint128>(
+      Span<const DpfKey* const>(kp1.data(), kp1.size()), pts, [&](Span<const uint128> v) {
+        std::memcpy(b.data(), v.data(), 16 * v.size());
+        return true;
+      });
+  bool ok = st.ok();
+  for (int i = 0; i < nkeys * per && ok; ++i)
+    ok = uint128(a[i] + b[i]) == (i % per == 0 ? betas[i / per] : uint128{0});
+  std::printf("{\"config\": \"c2a\", \"api\": \"C++ EvaluateAndApply<uint128>, 2^20 (key, point) "
+              "pairs over 64 keys\", \"points\": %d, \"best_ms\": %.3f, \"points_per_s\": %.4g, "
+              "\"correct\": %s}\n",
+              nkeys * per, 1e3 * best, nkeys * per / best, ok ? "true" : "false");
+}
+
+void C4(int reps) {
+  const int64_t n = int64_t{1} << 26;
+  const int rec = 256;
+  std::vector<char> data(static_cast<size_t>(n) * rec);
+  uint64_t x = 0x9e3779b97f4a7c15ull;
+  for (size_t i = 0; i < data.size(); i += 8) {  // splitmix64 records
+    uint64_t z = (x += 0x9e3779b97f4a7c15ull);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    z ^= z >> 31;
+    std::memcpy(&data[i], &z, 8);
+  }
+  PirConfig cfg;
+  cfg.mutable_dense_dpf_pir_config()->set_num_elements(n);
+  std::unique_ptr<DenseDpfPirServer> servers[2];
+  double build_s = 0;
+  for (int s = 0; s < 2; ++s) {
+    const double t0 = Now();
+    DenseDpfPirDatabase::Builder b;
+    b.InsertFixed(data.data(), n, rec);
+    auto db = b.Build();
+    OK_OR_DIE(db);
+    auto server = DenseDpfPirServer::CreatePlain(cfg, std::move(*db));
+    OK_OR_DIE(server);
+    servers[s] = std::move(*server);
+    build_s = Now() - t0;
+  }
+  DpfParameters p;
+  p.set_log_domain_size(26);
+  p.mutable_value_type()->mutable_xor_wrapper()->set_bitsize(128);
+  auto dpf = DistributedPointFunction::Create(p);
+  OK_OR_DIE(dpf);
+  std::mt19937_64 rng(4);
+  for (int q : {1, 8, 64}) {
+    PirRequest req[2];
+    std::vector<int64_t> idx(q);
+    for (int k = 0; k < q; ++k) {
+      idx[k] = static_cast<int64_t>(rng() % n);
+      auto keys = (*dpf)->GenerateKeys(
+          uint128(idx[k] / 128), XorWrapper<uint128>(uint128{1} << (idx[k] % 128)));
+      OK_OR_DIE(keys);
+      *req[0].mutable_dpf_pir_request()->mutable_plain_request()->add_dpf_key() = keys->first;
+      *req[1].mutable_dpf_pir_request()->mutable_plain_request()->add_dpf_key() = keys->second;
+    }
+    double best = 1e30, total = 0;
+    for (int r = 0; r <= reps; ++r) {
+      const double t0 = Now();
+      auto resp = servers[0]->HandleRequest(req[0]);
+      const double t = Now() - t0;
+      OK_OR_DIE(resp);
+      if (r > 0) {
+        best = std::min(best, t);
+        total += t;
+      }
+    }
+    auto r0 = servers[0]->HandleRequest(req[0]);
+    auto r1 = servers[1]->HandleRequest(req[1]);
+    OK_OR_DIE(r0);
+    OK_OR_DIE(r1);
+    bool ok = true;
+    for (int k = 0; k < q; ++k) {
+      const std::string& a = r0->dpf_pir_response().masked_response(k);
+      const std::string& b = r1->dpf_pir_response().masked_response(k);
+      for (int j = 0; j < rec && ok; ++j) ok = (a[j] ^ b[j]) == data[idx[k] * rec + j];
+    }
+    std::printf("{\"config\": \"c4\", \"api\": \"C++ DenseDpfPirServer::HandleRequest\", "
+                "\"records\": %lld, \"record_bytes\": %d, \"queries\": %d, \"best_ms\": %.3f, "
+                "\"mean_ms\": %.3f, \"db_GBps\": %.1f, \"build_s\": %.2f, \"correct\": %s}\n",
+                static_cast<long long>(n), rec, q, 1e3 * best, 1e3 * total / reps,
+                n * rec / best / 1e9, build_s, ok ? "true" : "false");
+    std::fflush(stdout);
+  }
 }
 
 void C3(int reps) {
@@ -220,8 +362,12 @@ void C3(int reps) {
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? std::atoi(argv[1]) : 5;
-  C1(reps);
-  C2(std::max(1, reps / 2));
-  C3(std::max(1, reps / 2));
+  const std::string only = argc > 2 ? argv[2] : "c1,c2,c2a,c3";
+  auto want = [&](const char* c) { return ("," + only + ",").find("," + std::string(c) + ",") != std::string::npos; };
+  if (want("c1")) C1(reps);
+  if (want("c2")) C2(std::max(1, reps / 2));
+  if (want("c2a")) C2Apply(std::max(1, reps / 2));
+  if (want("c3")) C3(std::max(1, reps / 2));
+  if (want("c4")) C4(reps);
   return 0;
 }
