@@ -5,6 +5,7 @@
 #include <string.h>
 
 #include <functional>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -277,13 +278,27 @@ int dpf_amd_evaluate_and_apply(const dpf_amd_dpf* dpf, const uint8_t* const* key
                                const uint64_t* points, int rightshift,
                                const uint8_t* value_type, size_t value_type_len, void* out,
                                dpf_amd_apply_fn op, void* user) {
-  std::vector<DpfKey> ks(num_keys);
+  // A key buffer passed for several points (same address and length) is
+  // parsed once, and the points share one DpfKey object (which the library
+  // uploads once).
+  std::vector<DpfKey> ks;
+  ks.reserve(num_keys);
   std::vector<const DpfKey*> ptrs(num_keys);
-  for (int64_t i = 0; i < num_keys; ++i) {
-    if (!ks[i].ParseFromArray(keys[i], key_lengths[i]))
-      return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed DpfKey proto");
-    ptrs[i] = &ks[i];
+  std::vector<int64_t> which(num_keys);
+  {
+    std::map<std::pair<const uint8_t*, size_t>, int64_t> parsed;
+    for (int64_t i = 0; i < num_keys; ++i) {
+      auto ins = parsed.emplace(std::make_pair(keys[i], key_lengths[i]),
+                                static_cast<int64_t>(ks.size()));
+      if (ins.second) {
+        ks.emplace_back();
+        if (!ks.back().ParseFromArray(keys[i], key_lengths[i]))
+          return Fail(DPF_AMD_INVALID_ARGUMENT, "malformed DpfKey proto");
+      }
+      which[i] = ins.first->second;
+    }
   }
+  for (int64_t i = 0; i < num_keys; ++i) ptrs[i] = &ks[which[i]];
   ValueType t;
   int rc = ParseType(value_type, value_type_len, &t);
   if (rc != DPF_AMD_OK) return rc;

@@ -1412,6 +1412,7 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
                                                const dpf_amd_value_type& layout,
                                                void* out) const {
   const DpfState& st = *state_;
+  HostTrace trace("EvaluateAt");
   if (ctx != nullptr && &key != &ctx->key())
     return InvalidArgumentError("`key` and `ctx->key()` must refer to the same object");
   if (hierarchy_level < 0) return InvalidArgumentError("`hierarchy_level` must be non-negative");
@@ -1435,6 +1436,7 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
   std::vector<uint128> corr;
   DPF_RETURN_IF_ERROR(CorrectionsFor(st, key, hierarchy_level, &corr));
   hipStream_t s = ThreadStream();
+  trace.Mark("validate");
 
   const int bbits = log_domain_size - m.tree_level;
   std::vector<uint128> tree(n);
@@ -1464,18 +1466,23 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
     const size_t bi_off = in_bytes;
     const size_t out_off = bi_off + (m.epb > 1 ? ((size_t(n) + 15) & ~size_t{15}) : 0);
     DeviceBuffer buf;
+    trace.Mark("prepare");
     DPF_RETURN_IF_ERROR(buf.Alloc(out_off + size_t(n) * vt.out_stride, s));
     char* d = buf.as<char>();
     DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 6, in_bytes, off, s));
     if (m.epb > 1) DPF_RETURN_IF_ERROR(ThreadUploadRing().Copy(d + bi_off, bidx.data(), n, s));
     DPF_RETURN_IF_ERROR(ClearPadding(vt, d + out_off, n * vt.out_stride, s));
+    trace.Mark("alloc+upload");
     DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_points_batched(
         1, n, d + off[1], reinterpret_cast<const uint8_t*>(d + off[5]), d + off[0], 0, levels,
         d + off[2], reinterpret_cast<const uint8_t*>(d + off[3]),
         reinterpret_cast<const uint8_t*>(d + off[4]), &vt,
         m.epb > 1 ? reinterpret_cast<const uint8_t*>(d + bi_off) : nullptr, nullptr,
         key.party(), nullptr, reinterpret_cast<const uint64_t*>(corr.data()), d + out_off, s)));
-    return CopyToHostSync(out, d + out_off, n * vt.out_stride, s);
+    trace.Mark("launch");
+    DPF_RETURN_IF_ERROR(CopyToHostSync(out, d + out_off, n * vt.out_stride, s));
+    trace.Mark("d2h+sync");
+    return OkStatus();
   }
   // With a context: the stored partial evaluations are walked to this
   // level's tree level first (EvaluateAt h:349-378 with ctx).
@@ -1512,30 +1519,73 @@ Status DistributedPointFunction::EvaluateAndApplyRaw(Span<const DpfKey* const> k
                                                      bool (*on_level)(void*, int),
                                                      void* user) const {
   const DpfState& st = *state_;
+  HostTrace trace("EvaluateAndApply");
   if (evaluation_points.size() != keys.size())
     return InvalidArgumentError("`keys.size()` != `evaluation_points.size()`");
-  for (size_t i = 0; i < keys.size(); ++i) DPF_RETURN_IF_ERROR(ValidateDpfKey(st, *keys[i]));
   const int64_t n = static_cast<int64_t>(keys.size());
   const int H = num_hierarchy_levels();
   *levels_done = 0;
   if (n == 0) return OkStatus();
-  hipStream_t s = ThreadStream();
-  std::vector<uint128> sv(n);
-  std::vector<uint8_t> cv(n);
-  std::vector<int8_t> party(n);
-  for (int64_t i = 0; i < n; ++i) {
-    sv[i] = MakeUint128(keys[i]->seed().high(), keys[i]->seed().low());
-    cv[i] = static_cast<uint8_t>(keys[i]->party() != 0);
-    party[i] = static_cast<int8_t>(keys[i]->party());
+  // The reference walks one seed per (key, point) pair with per-seed
+  // correction words (h:1101-1134, evaluate_prg_hwy.cc:264-301).  Callers
+  // pass the same key object for many points (a DCF batch, 64 keys x 2^14
+  // points at c2), so keys are deduplicated by address: every distinct key
+  // is validated and uploaded once, and each point carries its key's index.
+  std::vector<int32_t> kidx(n);
+  std::vector<const DpfKey*> uniq;
+  {
+    std::unordered_map<const DpfKey*, int32_t> seen;
+    const DpfKey* prev = nullptr;
+    int32_t prev_i = -1;
+    for (int64_t i = 0; i < n; ++i) {
+      const DpfKey* k = keys[i];
+      if (k != prev) {
+        auto ins = seen.emplace(k, static_cast<int32_t>(uniq.size()));
+        if (ins.second) uniq.push_back(k);
+        prev = k;
+        prev_i = ins.first->second;
+      }
+      kidx[i] = prev_i;
+    }
   }
-  DeviceBuffer seeds, cbs, paths, pty, dout;
-  DPF_RETURN_IF_ERROR(seeds.Upload(sv.data(), 16 * n, s));
-  DPF_RETURN_IF_ERROR(cbs.Upload(cv.data(), n, s));
+  for (const DpfKey* k : uniq) DPF_RETURN_IF_ERROR(ValidateDpfKey(st, *k));
+  const int64_t U = static_cast<int64_t>(uniq.size());
+  trace.Mark("dedup+validate");
+  hipStream_t s = ThreadStream();
+  std::vector<uint128> sv(U);
+  std::vector<uint8_t> cv(U);
+  std::vector<int8_t> party(U);
+  for (int64_t k = 0; k < U; ++k) {
+    sv[k] = MakeUint128(uniq[k]->seed().high(), uniq[k]->seed().low());
+    cv[k] = static_cast<uint8_t>(uniq[k]->party() != 0);
+    party[k] = static_cast<int8_t>(uniq[k]->party());
+  }
+  // Per-point inputs: the paths and key indices (the walk state lives in
+  // `state` between hierarchy levels, one seed + control bit per point).
+  DeviceBuffer key_seeds, key_cbs, paths, kix, pty, state, state_cb, dout;
+  DPF_RETURN_IF_ERROR(key_seeds.Upload(sv.data(), 16 * U, s));
+  DPF_RETURN_IF_ERROR(key_cbs.Upload(cv.data(), U, s));
+  DPF_RETURN_IF_ERROR(pty.Upload(party.data(), U, s));
   DPF_RETURN_IF_ERROR(paths.Upload(evaluation_points.data(), 16 * n, s));
-  DPF_RETURN_IF_ERROR(pty.Upload(party.data(), n, s));
+  DPF_RETURN_IF_ERROR(kix.Upload(kidx.data(), 4 * n, s));
+  if (H > 1) {
+    DPF_RETURN_IF_ERROR(state.Alloc(16 * n, s));
+    DPF_RETURN_IF_ERROR(state_cb.Alloc(n, s));
+  }
+  // Output buffer of the widest level (levels are evaluated one at a time).
+  size_t max_stride = 0;
+  for (int h = 0; h < H; ++h) {
+    dpf_amd_value_type vt;
+    DPF_RETURN_IF_ERROR(MergeLayout(st.levels[h], layout, &vt));
+    max_stride = std::max<size_t>(max_stride, vt.out_stride);
+  }
+  DPF_RETURN_IF_ERROR(dout.Alloc(n * max_stride, s));
+  trace.Mark("upload");
   const int last_ld = st.parameters.back().log_domain_size();
   int start_level = 0, stop_level = st.hierarchy_to_tree[0];
   char* host_out = static_cast<char*>(out);
+  std::vector<uint128> tmp;
+  std::vector<uint8_t> bidx;
   for (int h = 0; h < H; ++h) {
     if (h > 0) {
       start_level = stop_level;
@@ -1547,41 +1597,53 @@ Status DistributedPointFunction::EvaluateAndApplyRaw(Span<const DpfKey* const> k
     const int domain_rs = rightshift + last_ld - m.log_domain;
     const int tree_rs = rightshift + last_ld - m.tree_level;
     const int levels = stop_level - start_level;
-    std::vector<uint128> cws(static_cast<size_t>(levels) * n);
-    std::vector<uint8_t> ccl(cws.size()), ccr(cws.size()), bidx(n, 0);
-    for (int l = 0; l < levels; ++l)
-      for (int64_t j = 0; j < n; ++j) {
-        const CorrectionWord& cw = keys[j]->correction_words(start_level + l);
-        cws[l * n + j] = MakeUint128(cw.seed().high(), cw.seed().low());
-        ccl[l * n + j] = cw.control_left();
-        ccr[l * n + j] = cw.control_right();
-      }
+    // correction words [key][level] and value corrections [key]
+    std::vector<uint128> cws(static_cast<size_t>(levels) * U);
+    std::vector<uint8_t> ccl(cws.size()), ccr(cws.size());
     const int per = m.epb * static_cast<int>(m.scalars.size());
-    std::vector<uint128> corr(static_cast<size_t>(per) * n);
-    std::vector<uint128> tmp;
-    const int bbits = m.log_domain - m.tree_level;
-    for (int64_t j = 0; j < n; ++j) {
-      DPF_RETURN_IF_ERROR(CorrectionsFor(st, *keys[j], h, &tmp));
-      std::copy(tmp.begin(), tmp.end(), corr.begin() + j * per);
-      if (m.epb > 1 && domain_rs < 128)
-        bidx[j] = static_cast<uint8_t>((evaluation_points[j] >> domain_rs) &
-                                       ((uint128{1} << bbits) - 1));
+    std::vector<uint128> corr(static_cast<size_t>(per) * U);
+    for (int64_t k = 0; k < U; ++k) {
+      for (int l = 0; l < levels; ++l) {
+        const CorrectionWord& cw = uniq[k]->correction_words(start_level + l);
+        cws[k * levels + l] = MakeUint128(cw.seed().high(), cw.seed().low());
+        ccl[k * levels + l] = cw.control_left();
+        ccr[k * levels + l] = cw.control_right();
+      }
+      DPF_RETURN_IF_ERROR(CorrectionsFor(st, *uniq[k], h, &tmp));
+      std::copy(tmp.begin(), tmp.end(), corr.begin() + k * per);
     }
-    DeviceBuffer dcws, dccl, dccr, dcorr, dbi;
-    DPF_RETURN_IF_ERROR(dcws.Upload(cws.data(), 16 * cws.size(), s));
-    DPF_RETURN_IF_ERROR(dccl.Upload(ccl.data(), ccl.size(), s));
-    DPF_RETURN_IF_ERROR(dccr.Upload(ccr.data(), ccr.size(), s));
-    DPF_RETURN_IF_ERROR(dcorr.Upload(corr.data(), 16 * corr.size(), s));
-    DPF_RETURN_IF_ERROR(dbi.Upload(bidx.data(), n, s));
-    DPF_RETURN_IF_ERROR(dout.Alloc(n * vt.out_stride, s));
+    const bool want_bidx = m.epb > 1 && domain_rs < 128;
+    if (want_bidx) {
+      const int bbits = m.log_domain - m.tree_level;
+      const uint128 bmask = (uint128{1} << bbits) - 1;
+      bidx.assign(n, 0);
+      for (int64_t j = 0; j < n; ++j)
+        bidx[j] = static_cast<uint8_t>((evaluation_points[j] >> domain_rs) & bmask);
+    }
+    using Part = UploadRing::HostPart;
+    const Part parts[4] = {{cws.data(), 16 * cws.size()},
+                           {ccl.data(), ccl.size()},
+                           {ccr.data(), ccr.size()},
+                           {corr.data(), 16 * corr.size()}};
+    size_t off[4];
+    const size_t in_bytes = UploadRing::PackedLayout(parts, 4, off);
+    DeviceBuffer lvl, dbi;
+    DPF_RETURN_IF_ERROR(lvl.Alloc(in_bytes, s));
+    char* d = lvl.as<char>();
+    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 4, in_bytes, off, s));
+    if (want_bidx) DPF_RETURN_IF_ERROR(dbi.Upload(bidx.data(), n, s));
     DPF_RETURN_IF_ERROR(ClearPadding(vt, dout.get(), n * vt.out_stride, s));
-    DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_points(
-        n, seeds.get(), cbs.as<uint8_t>(), paths.get(), std::min(tree_rs, 255), levels,
-        static_cast<int64_t>(levels) * n, dcws.get(), dccl.as<uint8_t>(), dccr.as<uint8_t>(),
-        &vt, dbi.as<uint8_t>(), pty.as<int8_t>(), 0, dcorr.get(), nullptr, dout.get(),
-        seeds.get(), cbs.as<uint8_t>(), s)));
+    const bool first = h == 0;
+    DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd::EvaluatePointsIndexed(
+        n, kix.as<int32_t>(), U, first ? key_seeds.get() : state.get(),
+        first ? key_cbs.as<uint8_t>() : state_cb.as<uint8_t>(), first, paths.get(),
+        std::min(tree_rs, 255), levels, d + off[0], reinterpret_cast<const uint8_t*>(d + off[1]),
+        reinterpret_cast<const uint8_t*>(d + off[2]), &vt,
+        want_bidx ? dbi.as<uint8_t>() : nullptr, pty.as<int8_t>(), d + off[3], dout.get(),
+        h + 1 < H ? state.get() : nullptr, h + 1 < H ? state_cb.as<uint8_t>() : nullptr, s)));
     DPF_RETURN_IF_ERROR(
         CopyToHostSync(host_out + h * n * vt.out_stride, dout.get(), n * vt.out_stride, s));
+    trace.Mark("level");
     *levels_done = h + 1;
     // h:1190-1196: stop as soon as `op` returns false (the remaining levels
     // are never evaluated)

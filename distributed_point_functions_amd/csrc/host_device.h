@@ -210,12 +210,12 @@ class MemcpyPool {
 
 // Device-to-host copy into pageable `dst`, complete on return.  A plain
 // hipMemcpy into pageable memory stages through the runtime's own small
-// pinned buffers one after the other; large copies here go through two
-// pinned 16 MiB chunks per thread, the DMA of chunk i + 1 overlapping the
+// pinned buffers one after the other; copies above 1 MiB here go through two
+// pinned 4 MiB chunks per thread, the DMA of chunk i + 1 overlapping the
 // host memcpy of chunk i (c3: 128 MiB per level).
 class D2HStaging {
  public:
-  static constexpr size_t kChunk = 16u << 20;
+  static constexpr size_t kChunk = 4u << 20;
   D2HStaging() = default;
   D2HStaging(const D2HStaging&) = delete;
   D2HStaging& operator=(const D2HStaging&) = delete;
@@ -229,12 +229,20 @@ class D2HStaging {
     }
   }
   Status Copy(char* dst, const char* src, size_t bytes, hipStream_t s) {
+    int dev = 0;
+    DPF_RETURN_IF_ERROR(HipStatus(hipGetDevice(&dev), "hipGetDevice"));
     for (int i = 0; i < 2; ++i) {
       if (!pin_[i])
         DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc(&pin_[i], kChunk, 0), "hipHostMalloc"));
-      if (!ev_[i])
+      if (ev_[i] && dev_[i] != dev) {  // events are recorded on streams of their device
+        (void)hipEventDestroy(ev_[i]);  // idle: every copy below ends synchronized
+        ev_[i] = nullptr;
+      }
+      if (!ev_[i]) {
         DPF_RETURN_IF_ERROR(
             HipStatus(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "hipEventCreate"));
+        dev_[i] = dev;
+      }
     }
     const size_t n = (bytes + kChunk - 1) / kChunk;
     auto len = [&](size_t i) { return std::min(kChunk, bytes - i * kChunk); };
@@ -257,10 +265,75 @@ class D2HStaging {
  private:
   void* pin_[2] = {nullptr, nullptr};
   hipEvent_t ev_[2] = {nullptr, nullptr};
+  int dev_[2] = {-1, -1};
 };
 
+// Host-to-device copy of pageable `src` through two pinned chunks per
+// thread: the host memcpy of chunk i + 1 (split over MemcpyPool) overlaps the
+// DMA of chunk i.  Returns once `src` has been read; the DMAs stay ordered on
+// `s` (a chunk buffer is refilled only after the event behind its last DMA).
+class H2DStaging {
+ public:
+  static constexpr size_t kChunk = 4u << 20;
+  H2DStaging() = default;
+  H2DStaging(const H2DStaging&) = delete;
+  H2DStaging& operator=(const H2DStaging&) = delete;
+  ~H2DStaging() {
+    for (int i = 0; i < 2; ++i) {
+      if (ev_[i]) {
+        (void)hipEventSynchronize(ev_[i]);
+        (void)hipEventDestroy(ev_[i]);
+      }
+      if (pin_[i]) (void)hipHostFree(pin_[i]);
+    }
+  }
+  Status Copy(char* dst, const char* src, size_t bytes, hipStream_t s) {
+    int dev = 0;
+    DPF_RETURN_IF_ERROR(HipStatus(hipGetDevice(&dev), "hipGetDevice"));
+    for (int i = 0; i < 2; ++i) {
+      if (!pin_[i])
+        DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc(&pin_[i], kChunk, 0), "hipHostMalloc"));
+      if (ev_[i] && dev_[i] != dev) {  // events are recorded on streams of their device
+        DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(ev_[i]), "h2d"));
+        (void)hipEventDestroy(ev_[i]);
+        ev_[i] = nullptr;
+      }
+      if (!ev_[i]) {
+        DPF_RETURN_IF_ERROR(
+            HipStatus(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "hipEventCreate"));
+        dev_[i] = dev;
+        used_[i] = false;
+      }
+    }
+    for (size_t off = 0; off < bytes; off += kChunk) {
+      const size_t n = std::min(kChunk, bytes - off);
+      const int b = next_;
+      next_ ^= 1;
+      if (used_[b]) DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(ev_[b]), "h2d"));
+      MemcpyPool::Get().Copy(static_cast<char*>(pin_[b]), src + off, n);
+      DPF_RETURN_IF_ERROR(
+          HipStatus(hipMemcpyAsync(dst + off, pin_[b], n, hipMemcpyHostToDevice, s), "h2d"));
+      DPF_RETURN_IF_ERROR(HipStatus(hipEventRecord(ev_[b], s), "hipEventRecord"));
+      used_[b] = true;
+    }
+    return OkStatus();
+  }
+
+ private:
+  void* pin_[2] = {nullptr, nullptr};
+  hipEvent_t ev_[2] = {nullptr, nullptr};
+  int dev_[2] = {-1, -1};
+  bool used_[2] = {false, false};
+  int next_ = 0;
+};
+
+inline H2DStaging& ThreadH2DStaging() {
+  thread_local H2DStaging staging;
+  return staging;
+}
+
 inline Status CopyToHostSync(void* dst, const void* src, size_t bytes, hipStream_t s) {
-  if (bytes < 2 * D2HStaging::kChunk) {
+  if (bytes <= (size_t{1} << 20)) {
     DPF_RETURN_IF_ERROR(CopyToHost(dst, src, bytes, s));
     return HipStatus(hipStreamSynchronize(s), "sync");
   }
@@ -286,9 +359,9 @@ inline Status ClearPadding(const dpf_amd_value_type& vt, void* p, size_t bytes, 
 // that go out of scope before the stream drains, so every upload is first
 // copied into a pinned slot (then a true async DMA); a slot is reused only
 // after the event recorded behind its copy.  Uploads above kMaxSlotBytes
-// (e.g. DCF BatchEvaluate's per-key correction words at 2^20 keys, ~0.5 GiB)
-// do not grow a slot: they are copied straight from the caller's memory and
-// the stream is drained before returning, so no thread keeps GBs of pinned
+// (EvaluateAndApply's 2^20 points, DCF BatchEvaluate's per-key correction
+// words) do not grow a slot: they go through the thread's two pinned
+// H2DStaging chunks, so no thread keeps more than 16 + 8 MiB of pinned
 // memory for the life of the process.
 class UploadRing {
  public:
@@ -328,11 +401,10 @@ class UploadRing {
     if (bytes > kMaxSlotBytes) {
       for (int i = 0; i < k; ++i)
         if (parts[i].bytes)
-          DPF_RETURN_IF_ERROR(HipStatus(
-              hipMemcpyAsync(static_cast<char*>(dst) + (off ? off[i] : 0), parts[i].p,
-                             parts[i].bytes, hipMemcpyHostToDevice, s),
-              "upload"));
-      return HipStatus(hipStreamSynchronize(s), "upload sync");
+          DPF_RETURN_IF_ERROR(ThreadH2DStaging().Copy(static_cast<char*>(dst) + (off ? off[i] : 0),
+                                                      static_cast<const char*>(parts[i].p),
+                                                      parts[i].bytes, s));
+      return OkStatus();
     }
     Slot& sl = slots_[next_];
     next_ = (next_ + 1) % kSlots;
@@ -395,7 +467,7 @@ class UploadRing {
     return m;
   }
   static constexpr int kSlots = 16;
-  static constexpr size_t kMaxSlotBytes = size_t{16} << 20;
+  static constexpr size_t kMaxSlotBytes = size_t{1} << 20;
   struct Slot {
     void* host = nullptr;
     void* dev = nullptr;  // device address of `host`
@@ -413,12 +485,16 @@ inline UploadRing& ThreadUploadRing() {
 }
 
 // Caching device allocator with stream-ordered reuse, on top of hipMalloc.
-// The library does not use hipMallocAsync: with ROCm 7.2's runtime its pool
-// handed EvaluateUntil memory that kernels saw with wrong contents (c3 at
-// 2^16 prefixes: gather offsets out of range, or a wrong share at alpha at
-// hierarchy level 5 — also with kernels and copies serialized), while the
-// same binary on ROCm 7.0's runtime and on plain hipMalloc was bit-exact
-// (tools/malloc_async_repro.cc reproduces the pattern outside the library).
+// The library does not use hipMallocAsync: under ROCm 7.2's runtime
+// (70226015) a device-to-host hipMemcpyAsync out of pool memory that was
+// freed with hipFreeAsync and handed out again returns wrong bytes, while
+// kernels on the same stream see the right contents.  tools/
+// malloc_async_repro.cc reproduces it without the library — one stream, the
+// allocation pattern of a c3 level: from the first reused 128 MiB block on,
+// 100 % of the copied elements are wrong on the host and 0 on the device
+// (profiles/malloc_async_repro_r03.log); hipMalloc: 0 wrong.  The library
+// with DPF_AMD_MALLOC_ASYNC=1 fails c3 the same way (level 2 share sum,
+// gather-offset check).
 // A freed block keeps an event recorded on the freeing stream; it is handed
 // out again at once on that stream (stream order covers the reuse) and on
 // any other stream once the event has completed.  Sizes are rounded to
@@ -608,8 +684,9 @@ class DeviceBuffer {
     Reset();
     stream_ = s;
     if (bytes == 0) bytes = 16;
-    Status st = NoPool() ? HipStatus(hipMalloc(&p_, bytes), "hipMalloc")
-                         : DevicePool::Get().Alloc(bytes, s, &p_);
+    Status st = MallocAsync() ? HipStatus(hipMallocAsync(&p_, bytes, s), "hipMallocAsync")
+                : NoPool()    ? HipStatus(hipMalloc(&p_, bytes), "hipMalloc")
+                              : DevicePool::Get().Alloc(bytes, s, &p_);
     if (st.ok() && LiveRanges::On()) LiveRanges::Get().Add(p_, bytes);
     return st;
   }
@@ -621,7 +698,9 @@ class DeviceBuffer {
   void Reset() {
     if (p_) {
       if (LiveRanges::On()) LiveRanges::Get().Remove(p_);
-      if (NoPool()) {
+      if (MallocAsync()) {
+        (void)hipFreeAsync(p_, stream_);
+      } else if (NoPool()) {
         (void)hipStreamSynchronize(stream_);
         (void)hipFree(p_);
       } else {
@@ -635,6 +714,13 @@ class DeviceBuffer {
   // of the caching pool.
   static bool NoPool() {
     static const bool on = std::getenv("DPF_AMD_NO_POOL") != nullptr;
+    return on;
+  }
+  // DPF_AMD_MALLOC_ASYNC=1 (diagnostics): the runtime's stream-ordered
+  // allocator (hipMallocAsync / hipFreeAsync on the buffer's stream), the
+  // allocator the DevicePool replaced (tools/malloc_async_repro.cc).
+  static bool MallocAsync() {
+    static const bool on = std::getenv("DPF_AMD_MALLOC_ASYNC") != nullptr;
     return on;
   }
   template <typename T>

@@ -80,4 +80,16 @@ int EvaluatePointsBatchedRange(int64_t num_keys, int64_t first_point, int64_t po
                                const int8_t* key_party, const void* key_value_corrections,
                                void* out, void* stream);
 
+// Point evaluation where point i belongs to key key_index[i] of num_keys
+// (EvaluateAndApply over key pointers with repeats): correction words
+// [key][level], key_party / key_value_corrections per key; starting seeds
+// per key (seeds_by_key) or per point.  Device pointers, stream-ordered.
+int EvaluatePointsIndexed(int64_t num_points, const int32_t* key_index, int64_t num_keys,
+                          const void* seeds, const uint8_t* control_bits, bool seeds_by_key,
+                          const void* paths, int paths_rightshift, int num_levels,
+                          const void* correction_seeds, const uint8_t* ccl, const uint8_t* ccr,
+                          const dpf_amd_value_type* vt, const uint8_t* block_index,
+                          const int8_t* key_party, const void* key_value_corrections, void* out,
+                          void* seeds_out, uint8_t* control_bits_out, void* stream);
+
 }  // namespace dpf_amd

@@ -69,20 +69,22 @@ template <int NP, class KeyMaker>
 __device__ __forceinline__ void WalkPoints(const WalkArgs& w, Walk<NP>& s, const KeyMaker& km,
                                            const Lds& L) {
   const int64_t ppk = w.points_per_key;
-  const bool per_seed = ppk == 0 && w.num_cw > w.num_levels;
+  const bool by_key = ppk > 0 || w.key_index != nullptr;
+  const bool per_seed = !by_key && w.num_cw > w.num_levels;
   const int64_t cw_step = per_seed ? w.num_seeds : 1;
   int64_t cw_base[NP];
   uint4 p[NP];
 #pragma unroll
   for (int n = 0; n < NP; ++n) {
-    s.src[n] = ppk > 0 ? s.idx[n] / ppk : s.idx[n];
-    cw_base[n] = ppk > 0 ? s.src[n] * w.num_levels : per_seed ? s.idx[n] : 0;
-    const uint4 v = w.seeds_in[s.src[n]];
+    s.src[n] = w.key_index ? (int64_t)w.key_index[s.idx[n]] : ppk > 0 ? s.idx[n] / ppk : s.idx[n];
+    cw_base[n] = by_key ? s.src[n] * w.num_levels : per_seed ? s.idx[n] : 0;
+    const int64_t si = (ppk > 0 || (w.key_index && w.seeds_by_key)) ? s.src[n] : s.idx[n];
+    const uint4 v = w.seeds_in[si];
     s.x[n][0] = v.x;
     s.x[n][1] = v.y;
     s.x[n][2] = v.z;
     s.x[n][3] = v.w;
-    s.t[n] = w.cb_in[s.src[n]];
+    s.t[n] = w.cb_in[si];
     if (w.paths) {
       p[n] = w.paths[s.idx[n]];
     } else {  // implicit paths: point j of each key is tree index j

@@ -78,6 +78,14 @@ struct WalkArgs {
   // implicit paths (paths == nullptr): point j of each key walks tree index
   // path_offset + j (a leaf range of a batched selection expansion)
   int64_t path_offset;
+  // Non-null: point i belongs to key key_index[i] (EvaluateAndApply over a
+  // span of key pointers with repeats); correction words [key][level],
+  // party and value corrections per key.  The walk's starting seeds are per
+  // key when seeds_by_key, else per point (a later hierarchy level resumes
+  // from the previous level's per-point seeds).
+  const int32_t* key_index;
+  int32_t seeds_by_key;
+  int32_t pad;
 };
 
 struct PointsArgs {

@@ -217,7 +217,7 @@ int dpf_amd_evaluate_seeds(int64_t num_seeds, int num_levels, int64_t num_correc
                                    hipMemcpyDeviceToDevice, st), "copy");
     return rc;
   }
-  WalkArgs a;
+  WalkArgs a{};
   a.path_offset = 0;
   a.num_seeds = num_seeds;
   a.num_cw = num_correction_words;
@@ -379,14 +379,15 @@ static int EvaluatePoints(int64_t num_points, int64_t points_per_key, int64_t nu
                           const uint8_t* block_index, const int8_t* party, int party_all,
                           const void* value_corrections, const uint64_t* value_correction_all,
                           void* out, void* seeds_out, uint8_t* control_bits_out,
-                          void* stream, int64_t path_offset = 0) {
+                          void* stream, int64_t path_offset = 0,
+                          const int32_t* key_index = nullptr, bool seeds_by_key = false) {
   if (num_points < 0 || num_levels < 0 || !vt)
     return SetError(DPF_AMD_INVALID_ARGUMENT, "bad arguments");
   if (num_points == 0) return DPF_AMD_OK;
   VtDev dev;
   int rc = MakeVtDev(*vt, value_correction_all, party_all, vt->elements_per_block, &dev);
   if (rc != DPF_AMD_OK) return rc;
-  PointsArgs a;
+  PointsArgs a{};
   a.w.num_seeds = num_points;
   a.w.num_cw = num_cw;
   a.w.seeds_in = (const uint4*)seeds;
@@ -401,6 +402,8 @@ static int EvaluatePoints(int64_t num_points, int64_t points_per_key, int64_t nu
   a.w.num_levels = num_levels;
   a.w.rightshift = paths_rightshift;
   a.w.path_offset = path_offset;
+  a.w.key_index = key_index;
+  a.w.seeds_by_key = seeds_by_key ? 1 : 0;
   a.block_index = block_index;
   a.party = party;
   a.value_corrections = (const uint4*)value_corrections;
@@ -518,6 +521,22 @@ int EvaluatePointsBatchedRange(int64_t num_keys, int64_t first_point, int64_t po
                         key_seeds, key_control_bits, nullptr, 0, num_levels, correction_seeds,
                         ccl, ccr, vt, nullptr, key_party, 0, key_value_corrections, nullptr, out,
                         nullptr, nullptr, stream, first_point);
+}
+
+int EvaluatePointsIndexed(int64_t num_points, const int32_t* key_index, int64_t num_keys,
+                          const void* seeds, const uint8_t* control_bits, bool seeds_by_key,
+                          const void* paths, int paths_rightshift, int num_levels,
+                          const void* correction_seeds, const uint8_t* ccl, const uint8_t* ccr,
+                          const dpf_amd_value_type* vt, const uint8_t* block_index,
+                          const int8_t* key_party, const void* key_value_corrections, void* out,
+                          void* seeds_out, uint8_t* control_bits_out, void* stream) {
+  if (num_points < 0 || num_keys < 0 || !key_index)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "bad indexed point evaluation");
+  if (num_points == 0) return DPF_AMD_OK;
+  return EvaluatePoints(num_points, 0, num_keys * num_levels, seeds, control_bits, paths,
+                        paths_rightshift, num_levels, correction_seeds, ccl, ccr, vt, block_index,
+                        key_party, 0, key_value_corrections, nullptr, out, seeds_out,
+                        control_bits_out, stream, 0, key_index, seeds_by_key);
 }
 }  // namespace dpf_amd
 

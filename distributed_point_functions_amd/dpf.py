@@ -326,7 +326,10 @@ class DistributedPointFunction:
         """EvaluateAndApply<T, Fn> (h:403-407): op(values) after each level."""
         vt = self._type(0, value_type)
         tp = vt.to_proto()
-        datas = [bytes(k) for k in keys]
+        # one serialization per key object: the library parses (and uploads)
+        # a key buffer passed for several points once
+        ser = {}
+        datas = [ser[id(k)] if id(k) in ser else ser.setdefault(id(k), bytes(k)) for k in keys]
         arr = (ctypes.c_char_p * max(len(datas), 1))(*datas)
         lens = (ctypes.c_size_t * max(len(datas), 1))(*[len(d) for d in datas])
         if len(points) != len(keys):

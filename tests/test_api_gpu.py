@@ -158,6 +158,43 @@ def test_evaluate_and_apply_matches_per_level_evaluate_at(api, lds):
             assert seen[h][i] == od.evaluate_at(ok, h, [prefix])[0][0], (h, i)
 
 
+@pytest.mark.parametrize("spec,lds", [(("int", 32), [4, 12, 20]), (("int", 128), [16, 128]),
+                                      (("xor", 128), [7, 19])])
+def test_evaluate_and_apply_repeated_keys(api, spec, lds):
+    """Many points per key object, interleaved and in runs (the library
+    uploads each distinct key once and indexes it per point), both parties,
+    every level against the oracle (h:1072-1198)."""
+    levels = [(ld, spec, 0) for ld in lds]
+    dpf = _make(api, levels)
+    od = po.Dpf(levels)
+    rng = random.Random(11)
+    top = (1 << lds[-1]) - 1
+    keys, okeys, alphas = [], [], []
+    for s in range(3):
+        alpha = rng.randrange(top + 1)
+        alphas += [alpha, alpha]
+        betas = [rng.randrange(1, 1 << 31) for _ in lds]
+        k = dpf.generate_keys_incremental(alpha, betas, seeds=(10 + s, 20 + s))
+        ok = od.generate_keys(alpha, betas, seeds=(10 + s, 20 + s))
+        keys += list(k)
+        okeys += list(ok)
+    order = [i % 6 for i in range(120)] + [j for j in range(6) for _ in range(40)]
+    head = order[:60]
+    rng.shuffle(head)
+    order[:60] = head
+    points = [rng.randrange(top + 1) for _ in order]
+    for i in range(0, len(points), 7):  # some points on their key's alpha path
+        points[i] = alphas[order[i]]
+    seen = []
+    dpf.evaluate_and_apply([keys[j] for j in order], points,
+                           lambda vals: seen.append(list(vals)) or True)
+    assert len(seen) == len(lds)
+    for h, ld in enumerate(lds):
+        shift = lds[-1] - ld
+        want = [od.evaluate_at(okeys[j], h, [p >> shift])[0][0] for j, p in zip(order, points)]
+        assert seen[h] == want, h
+
+
 def test_evaluate_and_apply_stops_when_op_returns_false(api):
     levels = [(8, ("int", 32), 48), (16, ("int", 32), 56)]
     dpf = _make(api, levels)
