@@ -109,6 +109,7 @@ def lib():
     _sig(L, "dpf_amd_xor_fold", I32, P, I32, I64, P, P)
     _sig(L, "dpf_amd_set_expand_depth", I32, I32)
     _sig(L, "dpf_amd_set_scan_m4", I32, I32)
+    _sig(L, "dpf_amd_set_walk_mode", I32, I32)
     _bind_tier2(L)
     _lib = L
     return L

@@ -723,6 +723,7 @@ using dpf_internal_host::CopyToHostSync;
 using dpf_internal_host::DeviceBuffer;
 using dpf_internal_host::HipStatus;
 using dpf_internal_host::HostTrace;
+using dpf_internal_host::HostPool;
 using dpf_internal_host::ThreadStream;
 using dpf_internal_host::StreamSyncGuard;
 using dpf_internal_host::ThreadUploadRing;
@@ -1066,6 +1067,99 @@ StatusOr<EvaluationContext> DistributedPointFunction::CreateEvaluationContext(Dp
 
 namespace {
 
+// Per-thread host scratch of the incremental path, kept across calls: at
+// 2^16 prefixes per level (c3) fresh vectors of a few MiB each cost more in
+// page faults than the loops that fill them.  The seeds / control bits live in
+// pinned memory, so the walked seeds come back by an asynchronous DMA.
+struct IncrementalScratch {
+  std::vector<int64_t> src;
+  uint128* tree = nullptr;   // pinned: unique tree indices (the walk's paths)
+  uint128* seeds = nullptr;  // pinned
+  uint8_t* cbs = nullptr;    // pinned
+  int* flag = nullptr;       // pinned: the gather's error flag (an async copy)
+  size_t cap = 0;
+  hipEvent_t done = nullptr;
+  int device = -1;
+  ~IncrementalScratch() {
+    if (done) {
+      (void)hipEventSynchronize(done);
+      (void)hipEventDestroy(done);
+    }
+    if (tree) (void)hipHostFree(tree);
+    if (seeds) (void)hipHostFree(seeds);
+    if (cbs) (void)hipHostFree(cbs);
+    if (flag) (void)hipHostFree(flag);
+  }
+  Status Reserve(size_t n) {
+    if (!flag) DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc((void**)&flag, 64, 0), "hipHostMalloc"));
+    int dev = 0;
+    DPF_RETURN_IF_ERROR(HipStatus(hipGetDevice(&dev), "hipGetDevice"));
+    if (done && device != dev) {  // events are recorded on streams of their device
+      (void)hipEventSynchronize(done);
+      (void)hipEventDestroy(done);
+      done = nullptr;
+    }
+    if (!done) {
+      DPF_RETURN_IF_ERROR(
+          HipStatus(hipEventCreateWithFlags(&done, hipEventDisableTiming), "hipEventCreate"));
+      device = dev;
+    }
+    if (n <= cap) return OkStatus();
+    if (tree) (void)hipHostFree(tree);
+    if (seeds) (void)hipHostFree(seeds);
+    if (cbs) (void)hipHostFree(cbs);
+    tree = nullptr;
+    seeds = nullptr;
+    cbs = nullptr;
+    cap = 0;
+    size_t c = 1024;
+    while (c < n) c <<= 1;
+    DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc((void**)&tree, 16 * c, 0), "hipHostMalloc"));
+    DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc((void**)&seeds, 16 * c, 0), "hipHostMalloc"));
+    DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc((void**)&cbs, c, 0), "hipHostMalloc"));
+    cap = c;
+    return OkStatus();
+  }
+};
+
+IncrementalScratch& ThreadScratch() {
+  thread_local IncrementalScratch s;
+  return s;
+}
+
+// The context rewrite of ComputePartialEvaluations, deferred: the walked
+// seeds come back by DMA behind the walk, and the caller rewrites `ctx`
+// (FinishContextUpdate) after it has queued the expansion, so the host work
+// overlaps the GPU's.
+struct PendingContextUpdate {
+  bool active = false;
+  Span<const uint128> prefixes;
+  int hierarchy_level = 0;
+};
+
+Status FinishContextUpdate(PendingContextUpdate& p, EvaluationContext& ctx) {
+  if (!p.active) return OkStatus();
+  p.active = false;
+  HostTrace trace("FinishContextUpdate");
+  IncrementalScratch& sc = ThreadScratch();
+  DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(sc.done), "d2h"));
+  trace.Mark("wait");
+  const int64_t n = static_cast<int64_t>(p.prefixes.size());
+  std::vector<PartialEvaluation>* pe = ctx.mutable_partial_evaluations();
+  pe->resize(n);
+  for (int64_t i = 0; i < n; ++i) {
+    PartialEvaluation& e = (*pe)[i];
+    e.mutable_prefix()->set_high(Uint128High64(p.prefixes[i]));
+    e.mutable_prefix()->set_low(Uint128Low64(p.prefixes[i]));
+    e.mutable_seed()->set_high(Uint128High64(sc.seeds[i]));
+    e.mutable_seed()->set_low(Uint128Low64(sc.seeds[i]));
+    e.set_control_bit(sc.cbs[i] != 0);
+  }
+  ctx.set_partial_evaluations_level(p.hierarchy_level);
+  trace.Mark("rewrite");
+  return OkStatus();
+}
+
 // ComputePartialEvaluations (cc:374-476): selects the stored partial
 // evaluations for `prefixes` (host map, as the reference's btree), walks them
 // on the device to `hierarchy_level`'s tree level, and rewrites ctx.
@@ -1075,13 +1169,22 @@ namespace {
 Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixes,
                                  int hierarchy_level, bool update_ctx, EvaluationContext& ctx,
                                  hipStream_t s, DeviceBuffer* buf, void** seeds_dev,
-                                 uint8_t** cb_dev) {
+                                 uint8_t** cb_dev, PendingContextUpdate* pending = nullptr) {
   HostTrace trace("PartialEvaluations");
   const int64_t n = static_cast<int64_t>(prefixes.size());
   int start_level = st.hierarchy_to_tree[ctx.partial_evaluations_level()];
   const int stop_level = st.hierarchy_to_tree[hierarchy_level];
-  std::unique_ptr<uint128[]> seeds(new uint128[n > 0 ? n : 1]);
-  std::unique_ptr<uint8_t[]> cbs(new uint8_t[n > 0 ? n : 1]);
+  IncrementalScratch& sc = ThreadScratch();
+  // prefixes already in the pinned scratch (EvaluateUntil's tree indices):
+  // the caller reserved it, and they go up by DMA without a host copy
+  const bool prefixes_pinned = prefixes.data() == sc.tree;
+  if (!prefixes_pinned) {
+    // a deferred DMA of an earlier call into the scratch must have landed
+    if (sc.done) DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(sc.done), "d2h"));
+    DPF_RETURN_IF_ERROR(sc.Reserve(n > 0 ? n : 1));
+  }
+  uint128* seeds = sc.seeds;
+  uint8_t* cbs = sc.cbs;
   if (ctx.partial_evaluations_size() > 0 && start_level <= stop_level) {
     const int shift = stop_level - start_level;
     const auto& pes = ctx.partial_evaluations();
@@ -1092,46 +1195,61 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
     auto query = [&](int64_t i) { return shift < 128 ? (prefixes[i] >> shift) : uint128{0}; };
     // Sorted fast path (the common case: prefixes come from a sorted
     // candidate list, and the stored evaluations are the previous call's
-    // sorted tree indices): one merge-join pass instead of the reference's
-    // btree, checking both orders on the way.  Anything it cannot decide
-    // (an unsorted side, a prefix it does not find) goes to the hash path,
-    // which also produces the reference's errors.
+    // sorted tree indices): a merge join instead of the reference's btree,
+    // split over the host pool (each query range binary-searches its start),
+    // checking both orders on the way.  The reference rejects a mismatching
+    // duplicate anywhere in the stored list (cc:390-405), so the merge
+    // result stands only if the whole list is strictly increasing (then it
+    // holds no duplicate at all).  Anything it cannot decide (an unsorted
+    // side, a prefix it does not find) goes to the hash path, which also
+    // produces the reference's errors.
     bool merged = m > 0;
-    {
-      int64_t j = 0;
-      uint128 pj = m > 0 ? pe_prefix(0) : 0, prev_q = 0;
-      for (int64_t i = 0; i < n && merged; ++i) {
-        const uint128 q = query(i);
-        if (i > 0 && q < prev_q) {
-          merged = false;
-          break;
+    HostPool& pool = HostPool::Get();
+    constexpr int kParts = static_cast<int>(HostPool::kWorkers) + 1;
+    bool ok[kParts];
+    if (merged) {
+      const int parts = pool.ParallelRanges(m, 8192, [&](int r, int64_t b, int64_t e) {
+        bool good = true;
+        for (int64_t k = std::max<int64_t>(b, 1); k < e; ++k)
+          good &= pe_prefix(k - 1) < pe_prefix(k);
+        ok[r] = good;
+      });
+      for (int r = 0; r < parts; ++r) merged &= ok[r];
+    }
+    if (merged && n > 0) {
+      const int parts = pool.ParallelRanges(n, 4096, [&](int r, int64_t b, int64_t e) {
+        ok[r] = true;
+        if (b >= e) return;
+        bool good = b == 0 || query(b - 1) <= query(b);
+        const uint128 q0 = query(b);
+        int64_t lo = 0, hi = m;  // first stored prefix >= q0
+        while (lo < hi) {
+          const int64_t mid = lo + (hi - lo) / 2;
+          if (pe_prefix(mid) < q0)
+            lo = mid + 1;
+          else
+            hi = mid;
         }
-        prev_q = q;
-        while (pj < q) {
-          if (++j == m) break;
-          const uint128 next = pe_prefix(j);
-          if (next <= pj) {
-            merged = false;
+        int64_t j = lo;
+        uint128 prev = q0;
+        for (int64_t i = b; i < e && good; ++i) {
+          const uint128 q = query(i);
+          if (q < prev) {
+            good = false;
             break;
           }
-          pj = next;
+          prev = q;
+          while (j < m && pe_prefix(j) < q) ++j;
+          if (j == m || pe_prefix(j) != q) {
+            good = false;
+            break;
+          }
+          seeds[i] = MakeUint128(pes[j].seed().high(), pes[j].seed().low());
+          cbs[i] = pes[j].control_bit() ? 1 : 0;
         }
-        if (!merged || j == m || pj != q) {
-          merged = false;
-          break;
-        }
-        seeds[i] = MakeUint128(pes[j].seed().high(), pes[j].seed().low());
-        cbs[i] = pes[j].control_bit() ? 1 : 0;
-      }
-      // The reference rejects a mismatching duplicate anywhere in the
-      // stored list (cc:390-405), not only where the queries reach: the
-      // merge result stands only if the rest of the list is strictly
-      // increasing too (then it holds no duplicate at all).
-      for (int64_t k = j + 1; k < m && merged; ++k) {
-        const uint128 next = pe_prefix(k);
-        if (next <= pj) merged = false;
-        pj = next;
-      }
+        ok[r] = good;
+      });
+      for (int r = 0; r < parts; ++r) merged &= ok[r];
     }
     if (!merged) {
       std::unordered_map<uint128, std::pair<uint128, bool>, U128Hash> prev;
@@ -1158,8 +1276,8 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
     }
   } else {
     const uint128 seed = MakeUint128(ctx.key().seed().high(), ctx.key().seed().low());
-    std::fill(seeds.get(), seeds.get() + n, seed);
-    std::fill(cbs.get(), cbs.get() + n, static_cast<uint8_t>(ctx.key().party() != 0));
+    std::fill(seeds, seeds + n, seed);
+    std::fill(cbs, cbs + n, static_cast<uint8_t>(ctx.key().party() != 0));
     start_level = 0;
   }
   trace.Mark("lookup");
@@ -1167,17 +1285,34 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
   CwArrays cw = KeyCws(ctx.key(), start_level, stop_level);
   const bool walk = levels > 0 && n > 0;
   using Part = UploadRing::HostPart;
-  const Part parts[6] = {{seeds.get(), size_t(16) * n},
-                         {cbs.get(), size_t(n)},
-                         {prefixes.data(), walk ? size_t(16) * n : 0},
-                         {cw.seeds.data(), walk ? size_t(16) * levels : 0},
-                         {cw.ccl.data(), walk ? size_t(levels) : 0},
-                         {cw.ccr.data(), walk ? size_t(levels) : 0}};
+  // correction words through the upload ring; the pinned seeds / control
+  // bits (and pinned prefixes) by direct DMA
+  const Part cw_parts[3] = {{cw.seeds.data(), walk ? size_t(16) * levels : 0},
+                            {cw.ccl.data(), walk ? size_t(levels) : 0},
+                            {cw.ccr.data(), walk ? size_t(levels) : 0}};
+  size_t cw_off[3];
+  const size_t cw_bytes = UploadRing::PackedLayout(cw_parts, 3, cw_off);
+  const Part parts[3] = {{seeds, size_t(16) * n},
+                         {cbs, size_t(n)},
+                         {prefixes.data(), walk ? size_t(16) * n : 0}};
   size_t off[6];
-  const size_t bytes = UploadRing::PackedLayout(parts, 6, off);
+  const size_t bytes = cw_bytes + UploadRing::PackedLayout(parts, 3, off);
+  for (int i = 0; i < 3; ++i) {
+    off[i] += cw_bytes;
+    off[3 + i] = cw_off[i];
+  }
   DPF_RETURN_IF_ERROR(buf->Alloc(bytes, s));
   char* d = buf->as<char>();
-  DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 6, bytes, off, s));
+  DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, cw_parts, 3, cw_bytes, cw_off, s));
+  for (int i = 0; i < 3; ++i) {
+    if (parts[i].bytes == 0) continue;
+    if (i < 2 || prefixes_pinned)
+      DPF_RETURN_IF_ERROR(HipStatus(
+          hipMemcpyAsync(d + off[i], parts[i].p, parts[i].bytes, hipMemcpyHostToDevice, s),
+          "upload"));
+    else
+      DPF_RETURN_IF_ERROR(ThreadUploadRing().Copy(d + off[i], parts[i].p, parts[i].bytes, s));
+  }
   *seeds_dev = d + off[0];
   *cb_dev = reinterpret_cast<uint8_t*>(d + off[1]);
   if (walk) {
@@ -1190,11 +1325,18 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
   trace.Mark("upload+walk_launch");
   ctx.clear_partial_evaluations();
   if (update_ctx && n > 0) {
-    StreamSyncGuard drain(s);  // no copy left in flight into seeds / cbs on an error
-    DPF_RETURN_IF_ERROR(CopyToHost(seeds.get(), *seeds_dev, 16 * n, s));
-    DPF_RETURN_IF_ERROR(CopyToHost(cbs.get(), *cb_dev, n, s));
-    DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
-    drain.Dismiss();
+    // seeds / cbs are pinned: the copies are true DMAs behind the walk
+    DPF_RETURN_IF_ERROR(CopyToHost(seeds, *seeds_dev, 16 * n, s));
+    DPF_RETURN_IF_ERROR(CopyToHost(cbs, *cb_dev, n, s));
+    DPF_RETURN_IF_ERROR(HipStatus(hipEventRecord(sc.done, s), "hipEventRecord"));
+    if (pending != nullptr) {
+      pending->active = true;
+      pending->prefixes = prefixes;
+      pending->hierarchy_level = hierarchy_level;
+      trace.Mark("d2h_queued");
+      return OkStatus();
+    }
+    DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(sc.done), "sync"));
     std::vector<PartialEvaluation>* pe = ctx.mutable_partial_evaluations();
     pe->resize(n);
     for (int64_t i = 0; i < n; ++i) {
@@ -1242,6 +1384,7 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
         return InvalidArgumentError("Index " + dpf_internal::U128ToString(p) +
                                     " out of range for hierarchy level " + std::to_string(prev_h));
   }
+  trace.Mark("range_check");
   const int log_domain_size = st.parameters[hierarchy_level].log_domain_size();
   if (log_domain_size - previous_log_domain_size > 62)
     return InvalidArgumentError(
@@ -1260,34 +1403,77 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   std::vector<uint128> corr;
   DPF_RETURN_IF_ERROR(CorrectionsFor(st, ctx.key(), hierarchy_level, &corr));
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ThreadStream();
+  trace.Mark("corrections");
 
-  // Unique tree indices in first-appearance order (h:772-796).  Sorted
-  // prefixes (the usual heavy-hitters candidate list) de-duplicate in one
-  // pass; otherwise a hash map stands in for the reference's btree.
-  std::vector<uint128> tree_indices;
-  std::vector<std::pair<int64_t, int>> prefix_map;
+  // Unique tree indices in first-appearance order (h:772-796), and each
+  // prefix's gather offset into the expansion (h:877-889).  Sorted prefixes
+  // (the usual heavy-hitters candidate list) de-duplicate in two parallel
+  // passes (count per range, then write); otherwise a hash map stands in for
+  // the reference's btree.
+  IncrementalScratch& sc = ThreadScratch();
+  // a DMA an earlier call left in flight into the scratch must have landed
+  if (sc.done) DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(sc.done), "d2h"));
+  DPF_RETURN_IF_ERROR(sc.Reserve(num_prefixes > 0 ? num_prefixes : 1));
+  uint128* tree_indices = sc.tree;
+  std::vector<int64_t>& src = sc.src;
+  int64_t num_unique = 0;
+  const int stop_level = st.hierarchy_to_tree[hierarchy_level];
+  const int start_level = prefixes.empty() ? 0 : st.hierarchy_to_tree[prev_h];
+  const int levels = stop_level - start_level;
+  const int cepb = 1 << (log_domain_size - stop_level);
+  // outputs of one tree index = 2^bbits prefixes x outputs_per_prefix, so
+  // every offset below is in range by construction
+  const int64_t seg = (int64_t{1} << levels) * cepb;
   if (!prefixes.empty()) {
     const int bbits = st.parameters[prev_h].log_domain_size() - st.hierarchy_to_tree[prev_h];
-    tree_indices.reserve(num_prefixes);
-    prefix_map.reserve(num_prefixes);
-    bool sorted = true;
-    for (int64_t i = 1; i < num_prefixes && sorted; ++i) sorted = prefixes[i - 1] <= prefixes[i];
-    if (sorted) {
-      for (int64_t i = 0; i < num_prefixes; ++i) {
-        const uint128 ti = prefixes[i] >> bbits;
-        const int bi = static_cast<int>(prefixes[i] & ((uint128{1} << bbits) - 1));
-        if (tree_indices.empty() || tree_indices.back() != ti) tree_indices.push_back(ti);
-        prefix_map.emplace_back(static_cast<int64_t>(tree_indices.size()) - 1, bi);
+    const uint64_t bmask = (uint64_t{1} << bbits) - 1;  // bbits <= 7 (epb <= 128)
+    if (static_cast<int64_t>(src.size()) < num_prefixes) src.resize(num_prefixes);
+    constexpr int kParts = static_cast<int>(HostPool::kWorkers) + 1;
+    int64_t count[kParts] = {}, first[kParts] = {};
+    bool ordered[kParts];
+    HostPool& pool = HostPool::Get();
+    const int parts = pool.ParallelRanges(num_prefixes, 8192, [&](int r, int64_t b, int64_t e) {
+      bool ok = true;
+      int64_t u = 0;
+      for (int64_t i = b; i < e; ++i) {
+        if (i == 0) {
+          ++u;
+          continue;
+        }
+        ok &= prefixes[i - 1] <= prefixes[i];
+        u += (prefixes[i] >> bbits) != (prefixes[i - 1] >> bbits);
       }
+      ordered[r] = ok;
+      count[r] = u;
+    });
+    bool sorted = true;
+    for (int r = 0; r < parts; ++r) {
+      sorted &= ordered[r];
+      first[r] = num_unique;
+      num_unique += count[r];
+    }
+    if (sorted) {
+      pool.ParallelRanges(num_prefixes, 8192, [&](int r, int64_t b, int64_t e) {
+        int64_t u = first[r];
+        for (int64_t i = b; i < e; ++i) {
+          const uint128 t = prefixes[i] >> bbits;
+          if (i == 0 || t != (prefixes[i - 1] >> bbits)) tree_indices[u++] = t;
+          src[i] = (u - 1) * seg +
+                   static_cast<int64_t>(static_cast<uint64_t>(prefixes[i]) & bmask) *
+                       outputs_per_prefix;
+        }
+      });
     } else {
+      num_unique = 0;
       std::unordered_map<uint128, int64_t, U128Hash> inverse;
       inverse.reserve(num_prefixes * 2);
       for (int64_t i = 0; i < num_prefixes; ++i) {
         const uint128 ti = prefixes[i] >> bbits;
-        const int bi = static_cast<int>(prefixes[i] & ((uint128{1} << bbits) - 1));
-        auto it = inverse.emplace(ti, static_cast<int64_t>(tree_indices.size()));
-        if (it.second) tree_indices.push_back(ti);
-        prefix_map.emplace_back(it.first->second, bi);
+        auto it = inverse.emplace(ti, num_unique);
+        if (it.second) tree_indices[num_unique++] = ti;
+        src[i] = it.first->second * seg +
+                 static_cast<int64_t>(static_cast<uint64_t>(prefixes[i]) & bmask) *
+                     outputs_per_prefix;
       }
     }
   }
@@ -1297,7 +1483,7 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   DeviceBuffer roots;
   void* root_seeds = nullptr;
   uint8_t* root_cb = nullptr;
-  int start_level = 0;
+  PendingContextUpdate pending;
   if (prefixes.empty()) {
     const uint128 seed = MakeUint128(ctx.key().seed().high(), ctx.key().seed().low());
     const uint8_t cb = static_cast<uint8_t>(ctx.key().party() != 0);
@@ -1311,29 +1497,27 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   } else {
     const bool update_ctx = hierarchy_level < L - 1;
     DPF_RETURN_IF_ERROR(ComputePartialEvaluations(
-        st, Span<const uint128>(tree_indices.data(), tree_indices.size()), prev_h, update_ctx,
-        ctx, s, &roots, &root_seeds, &root_cb));
-    start_level = st.hierarchy_to_tree[prev_h];
+        st, Span<const uint128>(tree_indices, num_unique), prev_h, update_ctx,
+        ctx, s, &roots, &root_seeds, &root_cb, &pending));
   }
   trace.Mark("partial_evaluations");
-  const int stop_level = st.hierarchy_to_tree[hierarchy_level];
-  const int levels = stop_level - start_level;
   CwArrays cw = KeyCws(ctx.key(), start_level, stop_level);
   DeviceBuffer cws, ccl, ccr;
   DPF_RETURN_IF_ERROR(cws.Upload(cw.seeds.data(), 16 * levels, s));
   DPF_RETURN_IF_ERROR(ccl.Upload(cw.ccl.data(), levels, s));
   DPF_RETURN_IF_ERROR(ccr.Upload(cw.ccr.data(), levels, s));
-  const int64_t num_roots = prefixes.empty() ? 1 : static_cast<int64_t>(tree_indices.size());
-  const int cepb = 1 << (log_domain_size - stop_level);
+  const int64_t num_roots = prefixes.empty() ? 1 : num_unique;
   const int64_t expanded = (num_roots << levels) * cepb;
   const size_t stride = static_cast<size_t>(vt.out_stride);
 
   DeviceBuffer staging, result, gather_err, src_dev;
-  int gather_flag = 0;
+  DPF_RETURN_IF_ERROR(sc.Reserve(1));
+  int* gather_flag = sc.flag;  // pinned: its copy does not wait for the kernels
+  *gather_flag = 0;
   // an error return must not leave the async D2H of gather_flag in flight
   StreamSyncGuard drain(s);
   void* gather_src_dev = nullptr;
-  std::vector<int64_t> gather_src_host;
+  const int64_t* gather_src_host = nullptr;
   void* expand_out = nullptr;
   if (prefixes.empty() && out_on_device) {
     expand_out = out;
@@ -1350,20 +1534,10 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   trace.Mark("expand_launch");
   void* final_dev = expand_out;
   if (!prefixes.empty()) {
-    // Per-prefix slices (h:877-889).
-    const int64_t blocks_per_tree_prefix = int64_t{1} << levels;
-    std::vector<int64_t> src(num_prefixes);
-    for (int64_t i = 0; i < num_prefixes; ++i)
-      src[i] = prefix_map[i].first * blocks_per_tree_prefix * cepb +
-               prefix_map[i].second * outputs_per_prefix;
-    for (int64_t i = 0; i < num_prefixes; ++i)
-      if (src[i] < 0 || src[i] > expanded - outputs_per_prefix)
-        return InternalError("gather offset " + std::to_string(src[i]) + " of prefix " +
-                             std::to_string(i) + " outside the " + std::to_string(expanded) +
-                             " expanded outputs");
+    // Per-prefix slices (h:877-889), offsets computed with the dedup above.
     DPF_RETURN_IF_ERROR(src_dev.Upload(src.data(), 8 * num_prefixes, s));
     gather_src_dev = src_dev.get();
-    gather_src_host = src;
+    gather_src_host = src.data();
     if (out_on_device) {
       final_dev = out;
     } else {
@@ -1375,13 +1549,16 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
     DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_gather_rows_checked(
         num_prefixes, src_dev.as<int64_t>(), outputs_per_prefix, stride, expand_out, expanded,
         final_dev, gather_err.as<int>(), s)));
-    DPF_RETURN_IF_ERROR(CopyToHost(&gather_flag, gather_err.get(), sizeof(int), s));
+    DPF_RETURN_IF_ERROR(CopyToHost(gather_flag, gather_err.get(), sizeof(int), s));
   }
+  // the context rewrite runs while the expansion and the gather do
+  DPF_RETURN_IF_ERROR(FinishContextUpdate(pending, ctx));
+  trace.Mark("ctx_rewrite");
   if (!out_on_device)
     DPF_RETURN_IF_ERROR(CopyToHostSync(out, final_dev, total * stride, s));
   else
     DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
-  if (gather_flag) {  // the offsets were checked on the host: the device copy differs
+  if (*gather_flag) {  // the offsets were checked on the host: the device copy differs
     std::string detail;
     if (!prefixes.empty()) {
       std::vector<int64_t> back(num_prefixes);

@@ -143,42 +143,68 @@ class StreamSyncGuard {
   hipStream_t s_;
 };
 
-// Host memcpy split over a few persistent worker threads: one thread copies
-// from pinned into pageable memory at ~8 GB/s, below the PCIe DMA rate.
-class MemcpyPool {
+// A few persistent host worker threads for the Tier-2 paths' data-parallel
+// host loops: Run(parts, fn) calls fn(0..parts-1) spread over the workers
+// and the caller and returns when all are done (one Run in flight at a
+// time; fn must not call Run).  One thread copies from pinned into pageable
+// memory at ~8 GB/s, below the PCIe DMA rate, and the incremental path's
+// per-prefix loops (2^16 per level at c3) are memory-bound the same way.
+class HostPool {
  public:
-  static MemcpyPool& Get() {
-    static MemcpyPool* pool = new MemcpyPool();  // never destroyed: workers live to exit
+  static constexpr size_t kWorkers = 7;
+  static HostPool& Get() {
+    static HostPool* pool = new HostPool();  // never destroyed: workers live to exit
     return *pool;
   }
-  void Copy(char* dst, const char* src, size_t bytes) {
-    const size_t parts = std::min<size_t>(kWorkers + 1, std::max<size_t>(1, bytes >> 20));
+  template <typename Fn>
+  void Run(size_t parts, const Fn& fn) {
     if (parts <= 1) {
-      std::memcpy(dst, src, bytes);
+      if (parts == 1) fn(size_t{0});
       return;
     }
-    std::lock_guard<std::mutex> one(call_mu_);  // one copy in flight at a time
-    const size_t per = (bytes + parts - 1) / parts;
+    std::lock_guard<std::mutex> one(call_mu_);
+    Job job{&fn, [](const void* f, size_t i) { (*static_cast<const Fn*>(f))(i); }};
     {
       std::lock_guard<std::mutex> l(mu_);
-      dst_ = dst;
-      src_ = src;
-      bytes_ = bytes;
-      per_ = per;
+      job_ = job;
       next_ = 1;
       parts_ = parts;
       pending_ = parts - 1;
       ++gen_;
     }
     cv_.notify_all();
-    std::memcpy(dst, src, std::min(per, bytes));  // part 0 on the caller
+    fn(size_t{0});  // part 0 on the caller
     std::unique_lock<std::mutex> l(mu_);
     done_cv_.wait(l, [&] { return pending_ == 0; });
   }
+  // Splits [0, n) into at most kWorkers + 1 ranges of at least `grain`.
+  // Returns the number of ranges (range i is fn's first argument).
+  template <typename Fn>
+  int ParallelRanges(int64_t n, int64_t grain, const Fn& fn) {
+    const int64_t parts =
+        std::max<int64_t>(1, std::min<int64_t>(kWorkers + 1, n / std::max<int64_t>(grain, 1)));
+    const int64_t per = (n + parts - 1) / parts;
+    Run(static_cast<size_t>(parts), [&](size_t i) {
+      const int64_t b = static_cast<int64_t>(i) * per;
+      fn(static_cast<int>(i), std::min(b, n), std::min(b + per, n));
+    });
+    return static_cast<int>(parts);
+  }
+  void Copy(char* dst, const char* src, size_t bytes) {
+    const size_t parts = std::min<size_t>(kWorkers + 1, std::max<size_t>(1, bytes >> 20));
+    const size_t per = (bytes + parts - 1) / parts;
+    Run(parts, [&](size_t i) {
+      const size_t off = i * per;
+      if (off < bytes) std::memcpy(dst + off, src + off, std::min(per, bytes - off));
+    });
+  }
 
  private:
-  static constexpr size_t kWorkers = 7;
-  MemcpyPool() {
+  struct Job {
+    const void* fn;
+    void (*call)(const void*, size_t);
+  };
+  HostPool() {
     for (size_t i = 0; i < kWorkers; ++i) std::thread([this] { Work(); }).detach();
   }
   void Work() {
@@ -189,12 +215,9 @@ class MemcpyPool {
       seen = gen_;
       while (next_ < parts_) {
         const size_t i = next_++;
-        const size_t off = i * per_;
-        char* d = dst_;
-        const char* sr = src_;
-        const size_t n = off < bytes_ ? std::min(per_, bytes_ - off) : 0;
+        const Job job = job_;
         l.unlock();
-        if (n) std::memcpy(d + off, sr + off, n);
+        job.call(job.fn, i);
         l.lock();
         if (--pending_ == 0) done_cv_.notify_one();
       }
@@ -202,9 +225,8 @@ class MemcpyPool {
   }
   std::mutex call_mu_, mu_;
   std::condition_variable cv_, done_cv_;
-  char* dst_ = nullptr;
-  const char* src_ = nullptr;
-  size_t bytes_ = 0, per_ = 0, next_ = 0, parts_ = 0, pending_ = 0;
+  Job job_{nullptr, nullptr};
+  size_t next_ = 0, parts_ = 0, pending_ = 0;
   uint64_t gen_ = 0;
 };
 
@@ -256,7 +278,7 @@ class D2HStaging {
       if (i >= 1) {
         const size_t j = i - 1;
         DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(ev_[j & 1]), "d2h"));
-        MemcpyPool::Get().Copy(dst + j * kChunk, static_cast<const char*>(pin_[j & 1]), len(j));
+        HostPool::Get().Copy(dst + j * kChunk, static_cast<const char*>(pin_[j & 1]), len(j));
       }
     }
     return OkStatus();
@@ -269,7 +291,7 @@ class D2HStaging {
 };
 
 // Host-to-device copy of pageable `src` through two pinned chunks per
-// thread: the host memcpy of chunk i + 1 (split over MemcpyPool) overlaps the
+// thread: the host memcpy of chunk i + 1 (split over HostPool) overlaps the
 // DMA of chunk i.  Returns once `src` has been read; the DMAs stay ordered on
 // `s` (a chunk buffer is refilled only after the event behind its last DMA).
 class H2DStaging {
@@ -310,7 +332,7 @@ class H2DStaging {
       const int b = next_;
       next_ ^= 1;
       if (used_[b]) DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(ev_[b]), "h2d"));
-      MemcpyPool::Get().Copy(static_cast<char*>(pin_[b]), src + off, n);
+      HostPool::Get().Copy(static_cast<char*>(pin_[b]), src + off, n);
       DPF_RETURN_IF_ERROR(
           HipStatus(hipMemcpyAsync(dst + off, pin_[b], n, hipMemcpyHostToDevice, s), "h2d"));
       DPF_RETURN_IF_ERROR(HipStatus(hipEventRecord(ev_[b], s), "hipEventRecord"));

@@ -244,6 +244,186 @@ __global__ __launch_bounds__(kPointsBlockOf<BN>, kPointsWavesOf<BN>) void KEvalu
   }
 }
 
+// ----------------------------------------------------------------------------
+// Quad-lane walk for launches too small to fill the chip
+// ----------------------------------------------------------------------------
+//
+// A point's walk is a chain of one AES per level (129 at log_domain 128), so
+// a launch of a few thousand points (one key's EvaluateAt: 16,384 points =
+// 256 waves, one per CU) runs at the latency of a lone wave's AES: the
+// 16 v_perm + 16 ds_read_b32 + 12 combine ops of a round issue back to back
+// from one wave (~350 cycles/round measured: 217 us per 129-level launch).
+// Here four lanes share a point, lane c holding column c of the state:
+// per round a lane forms its column from its own byte 0 and bytes 1-3 of the
+// next three columns (three quad_perm DPP moves), i.e. 4 lookups + 3 moves +
+// 5 VALU instead of 16 + 28, and the launch has four times the waves.  Round
+// keys are per column, so each lane keeps its column's words of the left key,
+// the left/right difference and the value key in registers (33 VGPRs).
+// Semantics are those of PointsIter (walk, value hash, emit) for BN <= 2.
+
+template <int SEL>
+__device__ __forceinline__ uint32_t QuadPerm(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, SEL, 0xf, 0xf, false);
+}
+constexpr int kQuadNext1 = 1 | (2 << 2) | (3 << 4) | (0 << 6);  // lane c <- c+1
+constexpr int kQuadNext2 = 2 | (3 << 2) | (0 << 4) | (1 << 6);  // lane c <- c+2
+constexpr int kQuadNext3 = 3 | (0 << 2) | (1 << 4) | (2 << 6);  // lane c <- c+3
+template <int K>
+constexpr int kQuadBcast = K | (K << 2) | (K << 4) | (K << 6);  // lane c <- K
+
+__device__ __forceinline__ uint32_t PickCol(int c, uint32_t a, uint32_t b, uint32_t d,
+                                            uint32_t e) {
+  return c == 0 ? a : c == 1 ? b : c == 2 ? d : e;
+}
+
+// Column c's words of one expanded key: the initial and last round-key word
+// and the rotr16 form of rounds 1-9 (the T-table combine's operand).
+struct QuadKey {
+  uint32_t rk0, rk10, rkr[9];
+};
+template <int W>
+__device__ __forceinline__ QuadKey MakeQuadKey(int c) {
+  QuadKey k;
+  k.rk0 = PickCol(c, kDpfKeys[W].rk[0], kDpfKeys[W].rk[1], kDpfKeys[W].rk[2], kDpfKeys[W].rk[3]);
+  k.rk10 = PickCol(c, kDpfKeys[W].rk[40], kDpfKeys[W].rk[41], kDpfKeys[W].rk[42],
+                   kDpfKeys[W].rk[43]);
+#pragma unroll
+  for (int r = 1; r < 10; ++r)
+    k.rkr[r - 1] = PickCol(c, kDpfKeys[W].rkr[4 * r], kDpfKeys[W].rkr[4 * r + 1],
+                           kDpfKeys[W].rkr[4 * r + 2], kDpfKeys[W].rkr[4 * r + 3]);
+  return k;
+}
+struct QuadDiff {
+  uint32_t d[11];
+};
+__device__ __forceinline__ QuadDiff MakeQuadDiff(int c) {
+  QuadDiff k;
+#pragma unroll
+  for (int r = 0; r < 11; ++r)
+    k.d[r] = PickCol(c, kDpfDiff.d[4 * r], kDpfDiff.d[4 * r + 1], kDpfDiff.d[4 * r + 2],
+                     kDpfDiff.d[4 * r + 3]);
+  return k;
+}
+
+// AES-128 of the quad's state (this lane: column word w); the key of lane
+// group = left key, XORed with the left/right difference where m = ~0.
+template <bool MASKED>
+__device__ __forceinline__ uint32_t AesQuad(uint32_t w, const QuadKey& k, const QuadDiff& d,
+                                            uint32_t m, const Lds& L) {
+  w ^= k.rk0;
+  if (MASKED) w ^= d.d[0] & m;
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    const uint32_t x1 = QuadPerm<kQuadNext1>(w), x2 = QuadPerm<kQuadNext2>(w),
+                   x3 = QuadPerm<kQuadNext3>(w);
+    const uint32_t t0 = LoadT0(L, w, 0), t1 = LoadT1(L, x1, 1), t2 = LoadT0(L, x2, 2),
+                   t3 = LoadT1(L, x3, 3);
+    w = Xor3(t0, t1, Rotl16(Xor3(t2, t3, k.rkr[r - 1])));
+    if (MASKED) w ^= d.d[r] & m;
+  }
+  const uint32_t x1 = QuadPerm<kQuadNext1>(w), x2 = QuadPerm<kQuadNext2>(w),
+                 x3 = QuadPerm<kQuadNext3>(w);
+  const uint32_t t0 = LoadT0(L, w, 0), t1 = LoadT0(L, x1, 1), t2 = LoadT0(L, x2, 2),
+                 t3 = LoadT1(L, x3, 3);
+  const uint32_t lo = __builtin_amdgcn_perm(t1, t0, 0x0c0c0501u);
+  const uint32_t hi = __builtin_amdgcn_perm(t3, t2, 0x07020c0cu);
+  w = Xor3(lo, hi, k.rk10);
+  if (MASKED) w ^= d.d[10] & m;
+  return w;
+}
+
+// sigma(x) (aes_128_fixed_key_hash.cc:75-78) by columns: (x2, x3, x0^x2, x1^x3).
+__device__ __forceinline__ uint32_t SigmaQuad(uint32_t x, int c) {
+  const uint32_t y = QuadPerm<kQuadNext2>(x);
+  return c >= 2 ? (x ^ y) : y;
+}
+
+template <int BN>
+__global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluatePointsQuad(PointsArgs a,
+                                                                                   VtDev vt) {
+  __shared__ uint32_t tab[kTabWords];
+  FillTables(tab);
+  __syncthreads();
+  const Lds L = MakeLds(tab);
+  const int c = threadIdx.x & 3;
+  const QuadKey kl = MakeQuadKey<0>(c), kv = MakeQuadKey<2>(c);
+  const QuadDiff kd = MakeQuadDiff(c);
+  const WalkArgs& w = a.w;
+  const int64_t ppk = w.points_per_key;
+  const bool by_key = ppk > 0 || w.key_index != nullptr;
+  const bool per_seed = !by_key && w.num_cw > w.num_levels;
+  const int64_t cw_step = per_seed ? w.num_seeds : 1;
+  const uint32_t* cw_words = reinterpret_cast<const uint32_t*>(w.cw_seed);
+  const int per_elem = vt.epb * vt.ns;
+  const int64_t T = ((int64_t)gridDim.x * blockDim.x) >> 2;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2; i < w.num_seeds;
+       i += T) {
+    const int64_t src = w.key_index ? (int64_t)w.key_index[i] : ppk > 0 ? i / ppk : i;
+    const int64_t cw_base = by_key ? src * w.num_levels : per_seed ? i : 0;
+    const int64_t si = (ppk > 0 || (w.key_index && w.seeds_by_key)) ? src : i;
+    uint32_t x = reinterpret_cast<const uint32_t*>(w.seeds_in)[si * 4 + c];
+    uint32_t t = w.cb_in[si];
+    uint4 p;
+    if (w.paths) {
+      p = w.paths[i];
+    } else {
+      const uint64_t j = (uint64_t)(ppk > 0 ? i - src * ppk : i) + (uint64_t)w.path_offset;
+      p = make_uint4((uint32_t)j, (uint32_t)(j >> 32), 0u, 0u);
+    }
+    for (int level = 0; level < w.num_levels; ++level) {
+      const uint32_t bit = PathBit(p, w.num_levels - level - 1 + w.rightshift);
+      const int64_t ci = cw_base + level * cw_step;
+      const uint32_t cws = cw_words[ci * 4 + c];
+      const uint32_t cl = w.ccl[ci], cr = w.ccr[ci];
+      const uint32_t sg = SigmaQuad(x, c);
+      const uint32_t st = AesQuad<true>(sg, kl, kd, 0u - bit, L);
+      x = st ^ sg ^ (cws & (0u - t));
+      const uint32_t lsb = QuadPerm<kQuadBcast<0>>(x) & 1u;
+      t = lsb ^ (t & (bit ? cr : cl));
+      if (c == 0) x &= ~1u;
+    }
+    if (w.seeds_out) {
+      reinterpret_cast<uint32_t*>(w.seeds_out)[i * 4 + c] = x;
+      if (c == 0) w.cb_out[i] = (uint8_t)t;
+    }
+    // value hash (HashExpandedSeeds, cc:523-547): blocks H_V(seed + j), a
+    // 128-bit add (a walk of zero levels leaves the key's seed, bit 0 set or
+    // not)
+    u128 W[BN];
+#pragma unroll
+    for (int j = 0; j < BN; ++j) {
+      uint32_t in = x;
+      if (j > 0) {
+        const u128 v = ((u128)QuadPerm<kQuadBcast<0>>(x) | ((u128)QuadPerm<kQuadBcast<1>>(x) << 32) |
+                        ((u128)QuadPerm<kQuadBcast<2>>(x) << 64) |
+                        ((u128)QuadPerm<kQuadBcast<3>>(x) << 96)) +
+                       (u128)j;
+        in = (uint32_t)(v >> (32 * c));
+      }
+      const uint32_t sg = SigmaQuad(in, c);
+      const uint32_t h = AesQuad<false>(sg, kv, kd, 0u, L) ^ sg;
+      const uint32_t h0 = QuadPerm<kQuadBcast<0>>(h), h1 = QuadPerm<kQuadBcast<1>>(h),
+                     h2 = QuadPerm<kQuadBcast<2>>(h), h3 = QuadPerm<kQuadBcast<3>>(h);
+      W[j] = (u128)h0 | ((u128)h1 << 32) | ((u128)h2 << 64) | ((u128)h3 << 96);
+    }
+    if (c != 0) continue;
+    const int bi = a.block_index ? a.block_index[i] : 0;
+    const int party = a.party ? a.party[src] : vt.party;
+    char* dst = a.out + i * (int64_t)vt.stride;
+    if (a.value_corrections) {
+      u128 corr[kMaxCorrections];
+      const uint4* c4 = a.value_corrections + src * per_elem;
+      for (int j = 0; j < per_elem; ++j) {
+        const uint4 cc = c4[j];
+        corr[j] = (u128)cc.x | ((u128)cc.y << 32) | ((u128)cc.z << 64) | ((u128)cc.w << 96);
+      }
+      EmitLeaf<BN>(vt, W, t != 0, party, corr, bi, bi + 1, [dst](int) { return dst; });
+    } else {
+      EmitLeaf<BN>(vt, W, t != 0, party, vt.corr, bi, bi + 1, [dst](int) { return dst; });
+    }
+  }
+}
+
 // Up to 8192 blocks: past one resident round the dispatcher back-fills CUs
 // that finish early (c2 batched: 1.69 ms at 8192 vs 1.82 ms capped at 512).
 // Threads walk a second point only beyond 8192 blocks' worth of points.
@@ -389,8 +569,29 @@ static void LaunchPoints(int64_t n, hipStream_t st, const PointsArgs& a, const V
   hipLaunchKernelGGL((KEvaluatePoints<BN>), dim3(grid), dim3(block), 0, st, a, vt);
 }
 
+template <int BN>
+static void LaunchPointsQuad(int64_t n, hipStream_t st, const PointsArgs& a, const VtDev& vt) {
+  const int block = WalkBlock(4 * n, kPointsBlock);
+  const int grid = (int)std::min<int64_t>(DPF_WALK_MAX_GRID, (4 * n + block - 1) / block);
+  hipLaunchKernelGGL((KEvaluatePointsQuad<BN>), dim3(grid), dim3(block), 0, st, a, vt);
+}
+
+// Points below which the quad-lane walk runs (one-chain lanes fill the chip
+// from ~2^18 points).
+#ifndef DPF_WALK_QUAD_MAX
+#define DPF_WALK_QUAD_MAX (1 << 16)
+#endif
+
 int LaunchEvaluatePoints(int bn, int64_t n, hipStream_t st, const PointsArgs& a,
                          const VtDev& vt) {
+  const int mode = WalkMode();  // 0 automatic, 1 quad-lane, 2 one lane per point
+  if (bn <= 2 && (mode == 1 || (mode == 0 && n <= DPF_WALK_QUAD_MAX))) {
+    if (bn == 1)
+      LaunchPointsQuad<1>(n, st, a, vt);
+    else
+      LaunchPointsQuad<2>(n, st, a, vt);
+    return LaunchCheck("evaluate_points kernel launch");
+  }
   switch (bn) {
     case 1:
       LaunchPoints<1>(n, st, a, vt);

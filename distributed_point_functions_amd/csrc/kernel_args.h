@@ -178,6 +178,8 @@ int LaunchExpandGeneric4(int D, int grid, hipStream_t st, const ExpandArgs& a, c
 int LaunchEvaluateSeeds(int64_t n, hipStream_t st, const WalkArgs& a, const KeyPair& kp);
 int LaunchEvaluatePoints(int bn, int64_t n, hipStream_t st, const PointsArgs& a,
                          const VtDev& vt);
+// The calling thread's point-walk kernel choice (dpf_amd_set_walk_mode).
+int WalkMode();
 int LaunchDcfEvaluate(int bn, hipStream_t st, const DcfArgs& a, const VtDev& vt);
 int LaunchAesMmo(int grid, hipStream_t st, const uint4* in, uint4* out, int64_t n,
                  const KeyPair& kp);

@@ -24,6 +24,7 @@ namespace {
 // Test hooks, per calling thread: a test forcing a kernel variant never
 // changes what another thread's launches pick.
 thread_local int t_expand_depth = 0;  // dpf_amd_set_expand_depth
+thread_local int t_walk_mode = 0;     // dpf_amd_set_walk_mode
 // dpf_amd_set_scan_m4; the process default comes from DPF_AMD_SCAN_M4 (A/B runs)
 const int kScanM4Default = [] {
   const char* e = std::getenv("DPF_AMD_SCAN_M4");
@@ -110,6 +111,8 @@ int LaunchExpandForType(int D, int grid, hipStream_t st, const ExpandArgs& a,
 }
 
 }  // namespace
+
+int WalkMode() { return t_walk_mode; }
 
 int MakeVtDev(const dpf_amd_value_type& vt, const uint64_t* correction, int party,
               int cepb, VtDev* out) {
@@ -361,6 +364,13 @@ int dpf_amd_set_expand_depth(int depth) {
     return -3;
   const int old = t_expand_depth;
   t_expand_depth = depth;
+  return old;
+}
+
+int dpf_amd_set_walk_mode(int mode) {
+  if (mode < 0 || mode > 2) return -2;
+  const int old = t_walk_mode;
+  t_walk_mode = mode;
   return old;
 }
 

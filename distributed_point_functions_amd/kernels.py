@@ -161,6 +161,25 @@ class forced_scan_m4:
         _lib.lib().dpf_amd_set_scan_m4(self.prev)
 
 
+class forced_walk_mode:
+    """Context manager selecting the point-walk kernel of this thread
+    (dpf_amd_set_walk_mode: 0 automatic, 1 four lanes per point, 2 one lane
+    per point)."""
+
+    def __init__(self, mode: int):
+        self.mode = mode
+
+    def __enter__(self):
+        prev = _lib.lib().dpf_amd_set_walk_mode(self.mode)
+        if prev < 0:
+            raise ValueError("walk mode must be 0, 1 or 2")
+        self.prev = prev
+        return self
+
+    def __exit__(self, *exc):
+        _lib.lib().dpf_amd_set_walk_mode(self.prev)
+
+
 def evaluate_points(seeds, control_bits, paths, paths_rightshift, num_levels,
                     cw_seeds, ccl, ccr, desc, block_index=None, party=None,
                     party_all: int = 0, value_corrections=None,

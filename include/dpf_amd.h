@@ -172,6 +172,14 @@ int dpf_amd_set_expand_depth(int depth);
  * Returns the previous setting, or -2 for an invalid mode (unchanged). */
 int dpf_amd_set_scan_m4(int mode);
 
+/* Test hook: the calling thread's point-walk kernel (EvaluateAt /
+ * EvaluateAndApply / the batched point evaluation).  0 = automatic (four
+ * lanes per point below 65,536 points for types of <= 256 bits, one lane per
+ * point above), 1 = four lanes per point whenever the type allows, 2 = one
+ * lane per point.  Returns the previous setting, or -2 for an invalid mode
+ * (unchanged). */
+int dpf_amd_set_walk_mode(int mode);
+
 /* Fused single-path evaluation: EvaluateSeeds from the given seeds along
  * `paths` (one AES per level, per-lane key select) + HashExpandedSeeds +
  * correction of element block_index[i] (EvaluateAtImpl h:1013-1063 and the

@@ -208,7 +208,10 @@ def test_expand_leaf_ranges(K, cuda):
 @pytest.mark.parametrize("spec", TYPES[:12] + [TYPES[13], TYPES[17]],
                          ids=[repr(t) for t in TYPES[:12] + [TYPES[13], TYPES[17]]])
 @pytest.mark.parametrize("ld", [0, 1, 2, 32, 128])
-def test_evaluate_points_matches_oracle(K, cuda, spec, ld):
+@pytest.mark.parametrize("walk", [1, 2], ids=["quad", "lane"])
+def test_evaluate_points_matches_oracle(K, cuda, spec, ld, walk):
+    """Both point-walk kernels (four lanes per point / one lane per point;
+    value types of more than 256 bits always take the latter)."""
     from distributed_point_functions_amd import value_types as vtm
     d, k0, k1, alpha, beta = _keys(spec, ld)
     vt = vtm.from_spec(spec)
@@ -224,12 +227,13 @@ def test_evaluate_points_matches_oracle(K, cuda, spec, ld):
         tree = [p >> bbits if epb > 1 else p for p in pts]
         bi = [p & ((1 << bbits) - 1) if epb > 1 else 0 for p in pts]
         n = len(pts)
-        out = K.evaluate_points(
-            K.u128_tensor([key.seed] * n, cuda), u8([key.party] * n, cuda),
-            K.u128_tensor(tree, cuda), 0, L, K.u128_tensor(key.cw_seeds()[:L], cuda),
-            u8(key.ccl()[:L], cuda), u8(key.ccr()[:L], cuda),
-            vt.descriptor(d.blocks_needed(0)), block_index=u8(bi, cuda),
-            party_all=key.party, value_correction_all=key.value_corrections()[0])
+        with K.forced_walk_mode(walk):
+            out = K.evaluate_points(
+                K.u128_tensor([key.seed] * n, cuda), u8([key.party] * n, cuda),
+                K.u128_tensor(tree, cuda), 0, L, K.u128_tensor(key.cw_seeds()[:L], cuda),
+                u8(key.ccl()[:L], cuda), u8(key.ccr()[:L], cuda),
+                vt.descriptor(d.blocks_needed(0)), block_index=u8(bi, cuda),
+                party_all=key.party, value_correction_all=key.value_corrections()[0])
         got = vt.decode_flat(out.cpu().numpy().view(vt.numpy_dtype()))
         assert got == want
 
@@ -239,7 +243,8 @@ def test_evaluate_points_matches_oracle(K, cuda, spec, ld):
                                                 TYPES[17])])
 @pytest.mark.parametrize("ld,nkeys,ppk", [(1, 3, 5), (32, 7, 37), (128, 4, 129),
                                           (20, 5, 70001)])
-def test_evaluate_points_batched_matches_oracle(K, cuda, spec, ld, nkeys, ppk):
+@pytest.mark.parametrize("walk", [0, 1, 2], ids=["auto", "quad", "lane"])
+def test_evaluate_points_batched_matches_oracle(K, cuda, spec, ld, nkeys, ppk, walk):
     """One launch over several keys (alternating parties) == the oracle's
     per-key EvaluateAt.  The last case has > 2^18 points, so threads walk two
     points each (the i / i + T pairing)."""
@@ -268,13 +273,15 @@ def test_evaluate_points_batched_matches_oracle(K, cuda, spec, ld, nkeys, ppk):
     ccl = [c for k in ks for c in (k.ccl()[:L] or [0])]
     ccr = [c for k in ks for c in (k.ccr()[:L] or [0])]
     import torch
-    out = K.evaluate_points_batched(
-        nkeys, ppk, K.u128_tensor([k.seed for k in ks], cuda), u8([k.party for k in ks], cuda),
-        K.u128_tensor(tree, cuda), 0, L, K.u128_tensor(cws, cuda), u8(ccl, cuda), u8(ccr, cuda),
-        vt.descriptor(d.blocks_needed(0)), block_index=u8(bi, cuda),
-        key_party=torch.tensor([k.party for k in ks], dtype=torch.int8, device=cuda),
-        key_value_corrections=K.u128_tensor(
-            [c for k in ks for c in k.value_corrections()[0]], cuda))
+    with K.forced_walk_mode(walk):
+        out = K.evaluate_points_batched(
+            nkeys, ppk, K.u128_tensor([k.seed for k in ks], cuda),
+            u8([k.party for k in ks], cuda), K.u128_tensor(tree, cuda), 0, L,
+            K.u128_tensor(cws, cuda), u8(ccl, cuda), u8(ccr, cuda),
+            vt.descriptor(d.blocks_needed(0)), block_index=u8(bi, cuda),
+            key_party=torch.tensor([k.party for k in ks], dtype=torch.int8, device=cuda),
+            key_value_corrections=K.u128_tensor(
+                [c for k in ks for c in k.value_corrections()[0]], cuda))
     got = vt.decode_flat(out.cpu().numpy().view(vt.numpy_dtype()))
     step = max(1, ppk // 300)
     for k in range(nkeys):
@@ -313,6 +320,10 @@ def test_evaluate_points_batched_implicit_paths(K, cuda, ld, nkeys, ppk):
                                          K.u128_tensor(list(range(ppk)) * nkeys, cuda), 0, L,
                                          *cw, desc, **rest)
     assert torch.equal(implicit, explicit)
+    for walk in (1, 2):  # both point-walk kernels
+        with K.forced_walk_mode(walk):
+            other = K.evaluate_points_batched(nkeys, ppk, *args, None, 0, L, *cw, desc, **rest)
+        assert torch.equal(implicit, other), walk
     got = implicit.cpu().numpy().view(np.uint64).reshape(nkeys, ppk, 2)
     for k in (0, nkeys - 1):
         full = keys[k][0].expand_subtree_words(ks[k], 0, L)
