@@ -91,6 +91,13 @@ def test_c2_full_size_batched_and_api_match_oracle(K, cuda):
         api = dpf.evaluate_at(keys[k][party_of[k]], 0, pts[k * per:(k + 1) * per], raw=True)
         a = api.view(np.uint64).reshape(-1, 2)
         assert np.array_equal(a, want[k * per:(k + 1) * per, 0, :]), k
+    # EvaluateAndApply<absl::uint128> over all 2^20 (key, point) pairs
+    # (h:1072-1198), each key object repeated for its 16,384 points (c2a)
+    seen = []
+    kl = [keys[k][party_of[k]] for k in range(nkeys) for _ in range(per)]
+    dpf.evaluate_and_apply(kl, pts, lambda v: seen.append(v) or True)
+    assert len(seen) == 1
+    assert seen[0] == [int(lo) | (int(hi) << 64) for lo, hi in want[:, 0, :]]
     # share sum at alpha (and 0 at a non-alpha point) with the other party
     for k in range(0, nkeys, 9):
         other = dpf.evaluate_at(keys[k][1 - party_of[k]], 0, pts[k * per:k * per + 9], raw=True)
