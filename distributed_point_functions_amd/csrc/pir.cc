@@ -291,6 +291,7 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
     hipEvent_t done = nullptr;
   };
   std::vector<Work> w(G);
+  dpf_internal_host::HostTrace trace("InnerProductSharded");
   const int dev0 = shards_[0].device;
   hipStream_t s0 = dpf_internal_host::ThreadStreamOn(dev0);
   void* gather = nullptr;
@@ -325,6 +326,7 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
       if (st.ok()) st = HipStatus(hipEventRecord(x.done, x.s), "hipEventRecord");
     }
   }
+  trace.Mark("selections+scan_launch");
   // 2. combine on the first shard's device: peer copies of the partials,
   // one XOR fold, one D2H
   const void* result = nullptr;
@@ -356,6 +358,7 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
                                     G == 1 ? w[0].s : s0),
                      "d2h");
   }
+  trace.Mark("combine_launch");
   // 3. drain every stream used, then return the buffers (no copy still reads them)
   for (size_t g = 0; g < G; ++g) {
     if (!w[g].s) continue;
@@ -376,6 +379,7 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
       if (p) DevicePool::Get().Free(p, w[g].s);
     if (w[g].done) (void)hipEventDestroy(w[g].done);
   }
+  trace.Mark("sync+free");
   if (!st.ok()) return st;
   std::vector<std::string> r(num_queries);
   for (int q = 0; q < num_queries; ++q) r[q].assign(host.data() + q * stride_, max_value_size_);
@@ -580,6 +584,7 @@ StatusOr<PirResponse> DenseDpfPirServer::HandlePlainRequest(const PirRequest& re
   if (plain.dpf_key_size() == 0) return InvalidArgumentError("`dpf_key` must not be empty");
   const int q = plain.dpf_key_size();
   std::vector<std::string> inner_products;
+  dpf_internal_host::HostTrace trace("HandlePlainRequest");
   const auto* gpu_db = dynamic_cast<const DenseDpfPirDatabase*>(database_.get());
   if (gpu_db != nullptr) {
     // Fused path: expand only the selection blocks the scan reads, straight
@@ -592,6 +597,7 @@ StatusOr<PirResponse> DenseDpfPirServer::HandlePlainRequest(const PirRequest& re
     const dpf_amd_value_type layout = dpf_internal::HostLayoutOf<XorWrapper<uint128>>();
     std::vector<const DpfKey*> keys(q);
     for (int i = 0; i < q; ++i) keys[i] = &plain.dpf_key(i);
+    trace.Mark("validate");
     auto fill = [&](const DenseDpfPirDatabase::Shard&, int64_t b0, int64_t b1, void* sel,
                     void* stream) -> Status {
       return dpf_->ExpandLeavesOnDeviceBatched(Span<const DpfKey* const>(keys.data(), keys.size()),
@@ -618,6 +624,7 @@ StatusOr<PirResponse> DenseDpfPirServer::HandlePlainRequest(const PirRequest& re
   PirResponse response;
   for (std::string& s : inner_products)
     *response.mutable_dpf_pir_response()->add_masked_response() = std::move(s);
+  trace.Mark("inner_products+response");
   return response;
 }
 

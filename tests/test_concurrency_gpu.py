@@ -19,15 +19,15 @@ pytestmark = pytest.mark.gpu
 THREADS = 1024
 
 
-def _run_threads(fn):
-    results, errors = [None] * THREADS, []
+def _run_threads(fn, threads_n=THREADS):
+    results, errors = [None] * threads_n, []
 
     def worker(t):
         try:
             results[t] = fn(t)
         except Exception as e:  # pragma: no cover - reported below
             errors.append(repr(e))
-    threads = [threading.Thread(target=worker, args=(t,)) for t in range(THREADS)]
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(threads_n)]
     for th in threads:
         th.start()
     for th in threads:
@@ -98,3 +98,40 @@ def test_pir_server_handle_request_from_1024_threads(cuda):
     for i, a, b in zip(idx, P.parse_response(want0), r1):
         assert bytes(x ^ y for x, y in zip(a, b)) == records[i].tobytes()
     assert all(_run_threads(lambda t: server.handle_request(req0) == want0))
+
+
+def test_incremental_and_evaluate_and_apply_from_128_threads(cuda):
+    """The incremental path's per-thread pinned scratch, the shared host
+    worker pool (prefix de-duplication and merge join split over it at
+    2^14+ prefixes) and the deferred context rewrite, plus EvaluateAndApply's
+    key de-duplication, from 128 concurrent threads: every thread's levels
+    and values equal the single-threaded ones."""
+    import random
+    from distributed_point_functions_amd import value_types as V
+    from distributed_point_functions_amd.dpf import DistributedPointFunction, DpfParameters
+    lds = [8, 16, 20]
+    dpf = DistributedPointFunction.create_incremental(
+        [DpfParameters(ld, V.Integer(64)) for ld in lds])
+    alpha = 0xABCDE
+    k0, k1 = dpf.generate_keys_incremental(alpha, [3, 4, 5], seeds=(21, 22))
+    rng = random.Random(128)
+    p1 = list(range(256))
+    p2 = sorted(set(rng.sample(range(1 << 16), 20000)) | {alpha >> 4})
+
+    def incremental():
+        ctx = dpf.create_evaluation_context(k0)
+        return [dpf.evaluate_next(p, ctx, raw=True).tobytes() for p in ([], p1, p2)]
+    want_inc = incremental()
+    keys = [k0, k1] * 3000
+    pts = [rng.randrange(1 << 20) for _ in keys]
+    pts[0] = alpha
+
+    def apply():
+        seen = []
+        dpf.evaluate_and_apply(keys, pts, lambda v: seen.append(v) or True)
+        return seen
+    want_apply = apply()
+
+    def call(t):
+        return incremental() == want_inc if t % 2 else apply() == want_apply
+    assert all(_run_threads(call, 128))
