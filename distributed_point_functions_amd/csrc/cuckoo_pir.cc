@@ -107,14 +107,7 @@ void Sha256(const std::string& a, const std::string& b, uint8_t out[32]) {
     for (int j = 0; j < 4; ++j) out[4 * i + j] = static_cast<uint8_t>(h[i] >> (24 - 8 * j));
 }
 
-hipStream_t CuckooStream() {
-  thread_local hipStream_t s = [] {
-    hipStream_t x = nullptr;
-    if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) x = nullptr;
-    return x;
-  }();
-  return s;
-}
+hipStream_t CuckooStream() { return dpf_internal_host::ThreadStream(); }
 
 Status HipStatus(hipError_t e, const char* what) {
   if (e == hipSuccess) return OkStatus();

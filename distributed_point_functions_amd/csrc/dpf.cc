@@ -1123,8 +1123,7 @@ struct IncrementalScratch {
 };
 
 IncrementalScratch& ThreadScratch() {
-  thread_local IncrementalScratch s;
-  return s;
+  return dpf_internal_host::ThreadRecycled<IncrementalScratch>::Get();
 }
 
 // The context rewrite of ComputePartialEvaluations, deferred: the walked

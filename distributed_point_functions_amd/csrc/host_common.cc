@@ -1,5 +1,9 @@
 // host_common.cc — error state and buffer management of the C ABI.
+#include <execinfo.h>
+#include <signal.h>
 #include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
 
 #include <string>
 
@@ -18,6 +22,42 @@ int SetError(int code, const std::string& message) {
 }
 
 const char* LastError() { return g_last_error.c_str(); }
+
+namespace {
+// DPF_AMD_SEGV_BACKTRACE=1 (diagnostics): on SIGSEGV / SIGBUS / SIGABRT
+// print the faulting thread's native stack to stderr (a host process's
+// Python faulthandler shows only Python frames), then hand the signal to
+// the previous handler.
+struct sigaction g_prev[32];
+void OnFatal(int sig, siginfo_t* info, void* uctx) {
+  char msg[128];
+  const int n = snprintf(msg, sizeof msg, "[dpf_amd] signal %d at address %p, thread stack:\n",
+                         sig, info ? info->si_addr : nullptr);
+  if (n > 0) (void)!write(2, msg, static_cast<size_t>(n));
+  void* frames[64];
+  const int k = backtrace(frames, 64);
+  backtrace_symbols_fd(frames, k, 2);
+  struct sigaction& prev = g_prev[sig];
+  if (prev.sa_flags & SA_SIGINFO) {
+    if (prev.sa_sigaction) prev.sa_sigaction(sig, info, uctx);
+  } else if (prev.sa_handler != SIG_IGN && prev.sa_handler != SIG_DFL) {
+    prev.sa_handler(sig);
+  } else {
+    signal(sig, SIG_DFL);
+    raise(sig);
+  }
+}
+const bool g_segv_trace = [] {
+  if (!getenv("DPF_AMD_SEGV_BACKTRACE")) return false;
+  struct sigaction sa;
+  memset(&sa, 0, sizeof sa);
+  sa.sa_sigaction = OnFatal;
+  sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+  sigemptyset(&sa.sa_mask);
+  for (int sig : {SIGSEGV, SIGBUS, SIGABRT}) sigaction(sig, &sa, &g_prev[sig]);
+  return true;
+}();
+}  // namespace
 
 }  // namespace dpf_amd
 

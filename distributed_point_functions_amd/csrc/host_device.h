@@ -39,21 +39,51 @@ inline Status AbiStatus(int rc) {
   return Status(static_cast<StatusCode>(rc), dpf_amd::LastError());
 }
 
-// The calling thread's stream, destroyed when the thread exits (a server
-// answering from many short-lived threads does not accumulate streams).
-inline hipStream_t ThreadStream() {
+// Per-thread host resources (streams, pinned staging buffers, events) are
+// recycled through a process-wide free list when their thread exits instead
+// of being destroyed: a server answering from many short-lived threads pays
+// for stream / pinned-memory creation once per concurrent thread, not once
+// per thread, and no HIP call runs in a thread-exit handler (destroying them
+// there — pinned frees and event syncs from dozens of exiting threads while
+// others launch work — is what the runtime crashed on in round 3's 128-thread
+// test).  Every recycled object waits for its own in-flight work before it
+// reuses a buffer, so a new owner thread inherits it safely.  The objects
+// are never destroyed (no HIP calls at process exit).
+template <class T>
+class ThreadRecycled {
+ public:
+  static T& Get() {
+    thread_local Holder h;
+    return *h.p;
+  }
+
+ private:
+  struct Pool {
+    std::mutex mu;
+    std::vector<T*> free;
+  };
+  static Pool& P() {
+    static Pool* p = new Pool();
+    return *p;
+  }
   struct Holder {
-    hipStream_t s = nullptr;
+    T* p = nullptr;
     Holder() {
-      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+      {
+        std::lock_guard<std::mutex> l(P().mu);
+        if (!P().free.empty()) {
+          p = P().free.back();
+          P().free.pop_back();
+        }
+      }
+      if (p == nullptr) p = new T();
     }
     ~Holder() {
-      if (s) (void)hipStreamDestroy(s);
+      std::lock_guard<std::mutex> l(P().mu);
+      P().free.push_back(p);
     }
   };
-  thread_local Holder h;
-  return h.s;
-}
+};
 
 // Makes `device` current for the guard's scope (the HIP runtime's current
 // device is per thread) and restores the previous one.
@@ -76,17 +106,11 @@ class DeviceGuard {
 
 // The calling thread's stream on `device` (sharded databases and multi-GPU
 // expansions issue each device's work on its own stream from one thread).
+struct ThreadStreams {
+  std::map<int, hipStream_t> s;
+};
 inline hipStream_t ThreadStreamOn(int device) {
-  struct Holder {
-    std::map<int, hipStream_t> s;
-    ~Holder() {
-      for (auto& kv : s) {
-        DeviceGuard g(kv.first);
-        (void)hipStreamDestroy(kv.second);
-      }
-    }
-  };
-  thread_local Holder h;
+  ThreadStreams& h = ThreadRecycled<ThreadStreams>::Get();
   auto it = h.s.find(device);
   if (it != h.s.end()) return it->second;
   DeviceGuard g(device);
@@ -94,6 +118,13 @@ inline hipStream_t ThreadStreamOn(int device) {
   if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
   h.s[device] = st;
   return st;
+}
+
+// The calling thread's stream on its current device.
+inline hipStream_t ThreadStream() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  return ThreadStreamOn(dev);
 }
 
 // Host-side phase timer: with DPF_AMD_TRACE_HOST set, Mark(name) prints the
@@ -349,18 +380,14 @@ class H2DStaging {
   int next_ = 0;
 };
 
-inline H2DStaging& ThreadH2DStaging() {
-  thread_local H2DStaging staging;
-  return staging;
-}
+inline H2DStaging& ThreadH2DStaging() { return ThreadRecycled<H2DStaging>::Get(); }
 
 inline Status CopyToHostSync(void* dst, const void* src, size_t bytes, hipStream_t s) {
   if (bytes <= (size_t{1} << 20)) {
     DPF_RETURN_IF_ERROR(CopyToHost(dst, src, bytes, s));
     return HipStatus(hipStreamSynchronize(s), "sync");
   }
-  thread_local D2HStaging staging;
-  return staging.Copy(static_cast<char*>(dst), static_cast<const char*>(src), bytes, s);
+  return ThreadRecycled<D2HStaging>::Get().Copy(static_cast<char*>(dst), static_cast<const char*>(src), bytes, s);
 }
 
 // Host layouts with holes (e.g. {uint32_t, uint64_t}: 16 bytes, 4 unused):
@@ -501,10 +528,7 @@ class UploadRing {
   int next_ = 0;
 };
 
-inline UploadRing& ThreadUploadRing() {
-  thread_local UploadRing ring;
-  return ring;
-}
+inline UploadRing& ThreadUploadRing() { return ThreadRecycled<UploadRing>::Get(); }
 
 // Caching device allocator with stream-ordered reuse, on top of hipMalloc.
 // The library does not use hipMallocAsync: under ROCm 7.2's runtime

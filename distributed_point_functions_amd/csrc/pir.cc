@@ -27,14 +27,7 @@ Status AbiStatus(int rc) {
   return Status(static_cast<StatusCode>(rc), dpf_amd::LastError());
 }
 
-hipStream_t PirStream() {
-  thread_local hipStream_t s = [] {
-    hipStream_t x = nullptr;
-    if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) x = nullptr;
-    return x;
-  }();
-  return s;
-}
+hipStream_t PirStream() { return dpf_internal_host::ThreadStream(); }
 
 // AlignBytes (pir/dense_dpf_pir_database.cc:40-52).
 int64_t AlignBytes(int64_t n) { return (n + 15) & ~int64_t{15}; }
