@@ -135,3 +135,39 @@ def test_incremental_and_evaluate_and_apply_from_128_threads(cuda):
     def call(t):
         return incremental() == want_inc if t % 2 else apply() == want_apply
     assert all(_run_threads(call, 128))
+
+
+def test_thread_resources_recycled_across_thread_generations(cuda):
+    """Per-thread streams, pinned staging and incremental scratch go back to
+    a free list when a thread exits and the next thread takes them over
+    (host_device.h ThreadRecycled): 6 generations of 48 short-lived threads
+    run EvaluateAt, a 2^14-prefix EvaluateNext (pinned scratch, host pool)
+    and an EvaluateAndApply with 2 MiB of points (pinned H2D staging), each
+    generation starting while nothing of the previous one is alive; every
+    result equals the single-threaded one."""
+    import random
+    from distributed_point_functions_amd import value_types as V
+    from distributed_point_functions_amd.dpf import DistributedPointFunction, DpfParameters
+    lds = [14, 18]
+    dpf = DistributedPointFunction.create_incremental(
+        [DpfParameters(ld, V.Integer(64)) for ld in lds])
+    k0, k1 = dpf.generate_keys_incremental(777, [9, 10], seeds=(31, 32))
+    rng = random.Random(6)
+    p1 = list(range(1 << 14))
+    pts = [rng.randrange(1 << 18) for _ in range(1 << 17)]
+    keys = [k0] * (len(pts) // 2) + [k1] * (len(pts) // 2)
+
+    def work(t):
+        kind = t % 3
+        if kind == 0:
+            return dpf.evaluate_at(k0, 1, pts[:5000], raw=True).tobytes()
+        if kind == 1:
+            ctx = dpf.create_evaluation_context(k1)
+            return [dpf.evaluate_next(p, ctx, raw=True).tobytes() for p in ([], p1)]
+        seen = []
+        dpf.evaluate_and_apply(keys, pts, lambda v: seen.append(v[::997]) or True)
+        return seen
+    want = [work(k) for k in range(3)]
+    for _ in range(6):
+        res = _run_threads(lambda t: work(t) == want[t % 3], 48)
+        assert all(res)
