@@ -280,6 +280,105 @@ __device__ __forceinline__ void Sigma(const uint32_t (&x)[4], uint32_t (&s)[4]) 
   s[3] = x[1] ^ x[3];
 }
 
+// ----------------------------------------------------------------------------
+// Quad-lane AES: four lanes share one state, lane c holding column c
+// (k_walk.hip KEvaluatePointsQuad, expand_device.h KExpandCoop's walk)
+// ----------------------------------------------------------------------------
+
+template <int SEL>
+__device__ __forceinline__ uint32_t QuadPerm(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, SEL, 0xf, 0xf, false);
+}
+constexpr int kQuadNext1 = 1 | (2 << 2) | (3 << 4) | (0 << 6);  // lane c <- c+1
+constexpr int kQuadNext2 = 2 | (3 << 2) | (0 << 4) | (1 << 6);  // lane c <- c+2
+constexpr int kQuadNext3 = 3 | (0 << 2) | (1 << 4) | (2 << 6);  // lane c <- c+3
+template <int K>
+constexpr int kQuadBcast = K | (K << 2) | (K << 4) | (K << 6);  // lane c <- K
+
+__device__ __forceinline__ uint32_t PickCol(int c, uint32_t a, uint32_t b, uint32_t d,
+                                            uint32_t e) {
+  return c == 0 ? a : c == 1 ? b : c == 2 ? d : e;
+}
+
+// Column c's words of one expanded key: the initial and last round-key word
+// and the rotr16 form of rounds 1-9 (the T-table combine's operand).
+struct QuadKey {
+  uint32_t rk0, rk10, rkr[9];
+};
+template <int W>
+__device__ __forceinline__ QuadKey MakeQuadKey(int c) {
+  QuadKey k;
+  k.rk0 = PickCol(c, kDpfKeys[W].rk[0], kDpfKeys[W].rk[1], kDpfKeys[W].rk[2], kDpfKeys[W].rk[3]);
+  k.rk10 = PickCol(c, kDpfKeys[W].rk[40], kDpfKeys[W].rk[41], kDpfKeys[W].rk[42],
+                   kDpfKeys[W].rk[43]);
+#pragma unroll
+  for (int r = 1; r < 10; ++r)
+    k.rkr[r - 1] = PickCol(c, kDpfKeys[W].rkr[4 * r], kDpfKeys[W].rkr[4 * r + 1],
+                           kDpfKeys[W].rkr[4 * r + 2], kDpfKeys[W].rkr[4 * r + 3]);
+  return k;
+}
+struct QuadDiff {
+  uint32_t d[11];
+};
+__device__ __forceinline__ QuadDiff MakeQuadDiff(int c) {
+  QuadDiff k;
+#pragma unroll
+  for (int r = 0; r < 11; ++r)
+    k.d[r] = PickCol(c, kDpfDiff.d[4 * r], kDpfDiff.d[4 * r + 1], kDpfDiff.d[4 * r + 2],
+                     kDpfDiff.d[4 * r + 3]);
+  return k;
+}
+
+// AES-128 of the quad's state (this lane: column word w); the key of lane
+// group = left key, XORed with the left/right difference where m = ~0.
+template <bool MASKED>
+__device__ __forceinline__ uint32_t AesQuad(uint32_t w, const QuadKey& k, const QuadDiff& d,
+                                            uint32_t m, const Lds& L) {
+  w ^= k.rk0;
+  if (MASKED) w ^= d.d[0] & m;
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    const uint32_t x1 = QuadPerm<kQuadNext1>(w), x2 = QuadPerm<kQuadNext2>(w),
+                   x3 = QuadPerm<kQuadNext3>(w);
+    const uint32_t t0 = LoadT0(L, w, 0), t1 = LoadT1(L, x1, 1), t2 = LoadT0(L, x2, 2),
+                   t3 = LoadT1(L, x3, 3);
+    w = Xor3(t0, t1, Rotl16(Xor3(t2, t3, k.rkr[r - 1])));
+    if (MASKED) w ^= d.d[r] & m;
+  }
+  const uint32_t x1 = QuadPerm<kQuadNext1>(w), x2 = QuadPerm<kQuadNext2>(w),
+                 x3 = QuadPerm<kQuadNext3>(w);
+  const uint32_t t0 = LoadT0(L, w, 0), t1 = LoadT0(L, x1, 1), t2 = LoadT0(L, x2, 2),
+                 t3 = LoadT1(L, x3, 3);
+  const uint32_t lo = __builtin_amdgcn_perm(t1, t0, 0x0c0c0501u);
+  const uint32_t hi = __builtin_amdgcn_perm(t3, t2, 0x07020c0cu);
+  w = Xor3(lo, hi, k.rk10);
+  if (MASKED) w ^= d.d[10] & m;
+  return w;
+}
+
+// sigma(x) (aes_128_fixed_key_hash.cc:75-78) by columns: (x2, x3, x0^x2, x1^x3).
+__device__ __forceinline__ uint32_t SigmaQuad(uint32_t x, int c) {
+  const uint32_t y = QuadPerm<kQuadNext2>(x);
+  return c >= 2 ? (x ^ y) : y;
+}
+
+// One level of a path walk by a quad (ExpandSeeds / EvaluateSeeds step,
+// cc:289-372): child = H_{bit}(sigma(x)) ^ sigma(x) ^ (t ? cw.seed : 0), its
+// control bit = LSB ^ (t & cw.control_{bit}), LSB cleared.  cw_word is
+// column c of the correction seed.
+__device__ __forceinline__ void QuadWalkStep(uint32_t& x, uint32_t& t, uint32_t bit,
+                                             uint32_t cw_word, uint32_t cl, uint32_t cr, int c,
+                                             const QuadKey& kl, const QuadDiff& kd,
+                                             const Lds& L) {
+  const uint32_t sg = SigmaQuad(x, c);
+  const uint32_t st = AesQuad<true>(sg, kl, kd, 0u - bit, L);
+  x = st ^ sg ^ (cw_word & (0u - t));
+  const uint32_t lsb = QuadPerm<kQuadBcast<0>>(x) & 1u;
+  t = lsb ^ (t & (bit ? cr : cl));
+  if (c == 0) x &= ~1u;
+}
+
+
 __device__ __forceinline__ u128 ToU128(const uint32_t (&x)[4]) {
   return (u128)x[0] | ((u128)x[1] << 32) | ((u128)x[2] << 64) | ((u128)x[3] << 96);
 }

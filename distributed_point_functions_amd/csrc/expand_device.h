@@ -407,9 +407,9 @@ int LaunchExpand(int, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
 // small launches cannot amortise (a 2^19-leaf launch at D = 2: 27 AES per 4
 // leaves against 12, and a 17-AES chain per thread).  Here a block owns a
 // 2^(10+E)-leaf subtree and computes every tree node of it once:
-//   1. wave 0 walks from the root to the block root (block-uniform path
-//      bits: one AES per level with the key chosen on the scalar unit) and
-//      on to 64 sub-roots six levels below (per-lane bits: masked keys);
+//   1. waves 0-3, as 64 quads of lanes sharing one AES state (lane c holds
+//      column c), walk from the root to the block root (block-uniform path
+//      bits) and on to 64 sub-roots six levels below, quad q to sub-root q;
 //   2. four breadth-first levels through LDS, one child per thread (a walk
 //      step with the key of the child's side): 64 -> 128 -> ... -> 1024;
 //   3. each thread hashes its node (E = 0) or expands it once more and
@@ -449,23 +449,31 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
   const int64_t root = kBatched ? key : chunk >> s;
   const uint64_t path = (uint64_t)chunk & ((s >= 63) ? ~0ull : ((1ull << s) - 1));
   const int64_t cw0 = kBatched ? key * a.num_levels : 0;
-  // 1. root -> block root -> 64 sub-roots (wave 0)
-  if (wave == 0) {
-    const uint4 rs = a.root_seeds[root];
-    uint32_t x[4] = {rs.x, rs.y, rs.z, rs.w};
+  // 1. root -> block root -> 64 sub-roots: waves 0-3 as 64 quads (four lanes
+  // per state, lane c holding column c: a lone chain's AES at a quarter of
+  // the lookups per lane), quad q walking to sub-root q; the walk to the
+  // block root is the same for every quad (block-uniform path bits).
+  if (wave < 4) {
+    const int c = lane & 3;
+    const int q = wave * 16 + (lane >> 2);
+    const QuadKey kl = MakeQuadKey<0>(c);
+    const QuadDiff kd = MakeQuadDiff(c);
+    const uint32_t* cw_words = reinterpret_cast<const uint32_t*>(a.cw_seed);
+    uint32_t x = reinterpret_cast<const uint32_t*>(a.root_seeds)[root * 4 + c];
     uint32_t t = a.root_cb[root];
+#pragma unroll 1
     for (int i = 0; i < s; ++i) {
       const uint32_t bit = (uint32_t)(path >> (s - 1 - i)) & 1u;  // block-uniform
-      const Cw cw = LoadCw(a.cw_seed, a.ccl, a.ccr, cw0 + i);
-      WalkStep(x, t, bit, cw, DpfSelect{{}, bit != 0}, L);
+      const int64_t ci = cw0 + i;
+      QuadWalkStep(x, t, bit, cw_words[ci * 4 + c], a.ccl[ci], a.ccr[ci], c, kl, kd, L);
     }
 #pragma unroll 1
     for (int i = 0; i < 6; ++i) {
-      const uint32_t bit = ((uint32_t)lane >> (5 - i)) & 1u;
-      const Cw cw = LoadCw(a.cw_seed, a.ccl, a.ccr, cw0 + s + i);
-      WalkStep(x, t, bit, cw, DpfMasked<1>{{0u - bit}}, L);
+      const uint32_t bit = ((uint32_t)q >> (5 - i)) & 1u;
+      const int64_t ci = cw0 + s + i;
+      QuadWalkStep(x, t, bit, cw_words[ci * 4 + c], a.ccl[ci], a.ccr[ci], c, kl, kd, L);
     }
-    nodes[lane] = make_uint4(x[0] | t, x[1], x[2], x[3]);
+    reinterpret_cast<uint32_t*>(nodes)[q * 4 + c] = c == 0 ? (x | t) : x;
   }
   __syncthreads();
   // 2. breadth-first: level j has 128 << j children, child c of parent c / 2

@@ -40,22 +40,26 @@ int GridFor(int64_t items, int block, int max_blocks) {
 }
 
 // Kernel for a single-key launch of `leaves` tree leaves of a tree of >= 11
-// levels, from tools/expand_sweep.py on MI355X (profiles/sweep_*_r03e.log):
-// below 2^20 leaves the launch is latency-bound (a 2^11-leaf, one-block
-// launch takes 27 us; 2^19 leaves: KExpandCoop 53-55 us, KExpand<2> 59,
-// KExpand<4> 112), and KExpandCoop computes each tree node once; from 2^20
-// on, KExpand<4>'s full-occupancy register DFS wins (2^21: 0.127 vs 0.143
-// ms; 2^23: 0.357 vs 0.549) until KExpand<8> at 2^25.
+// levels, from tools/expand_sweep.py on MI355X (profiles/sweep_*_r03i.log,
+// KExpandCoop with its quad-lane walk to the block root): below 2^22 leaves
+// the launch is latency-bound (one block of 2^11 leaves takes 22 us with the
+// launch) and KExpandCoop computes each tree node once — 2^19 leaves (c1, a
+// PIR selection): 38 us against KExpand<2> 59 and KExpand<4> 111; 2^21:
+// E = 1 0.108 ms against KExpand<4> 0.125; from 2^23 KExpand<4>'s
+// full-occupancy register DFS wins (0.358 vs 0.384 ms) until KExpand<8> at
+// 2^25.
 int CoopDepth(int64_t leaves) { return leaves >= (int64_t{1} << 19) ? -2 : -1; }
+constexpr int64_t kCoopMaxLeaves = int64_t{1} << 22;
 
 // Kernel for a batched expansion of num_keys x range tree leaves
-// (tools/expand_sweep.py batched): KExpand<4> with per-lane keys from 2^22
-// leaves in total (64 keys x 2^19: 1.26 ms = 0.65 of the LDS bound; the
-// cooperative kernel 1.90, KExpand<8> 1.34), KExpandCoop with per-block
-// keys below.
+// (tools/expand_sweep.py batched): KExpand<4> with per-lane keys from 2^23
+// leaves in total (16 keys x 2^19: 0.368 ms against the cooperative 0.408;
+// 64 keys x 2^19: 1.27 ms = 0.65 of the LDS bound, cooperative 1.41),
+// KExpandCoop with per-block keys below (8 x 2^19: 0.213 vs 0.215; 100 x
+// 2^16: 0.315 vs 0.346).
 int BatchedDepth(int64_t num_keys, int64_t range) {
   const int64_t total = num_keys * range;
-  if (total >= (int64_t{1} << 22) && range >= 16) return 4;
+  if (total >= (int64_t{1} << 23) && range >= 16) return 4;
   return CoopDepth(total);
 }
 
@@ -283,7 +287,7 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
   // Below 2^25 tree leaves the cooperative kernel computes every tree node
   // once per block instead of one root walk per thread (KExpandCoop,
   // expand_device.h): D = -1 (1024 leaves per block) or -2 (2048).
-  if (num_levels >= 11 && range < (int64_t{1} << 20)) D = CoopDepth(range);
+  if (num_levels >= 11 && range < kCoopMaxLeaves) D = CoopDepth(range);
   const int forced = t_expand_depth;
   if (forced > 0 && forced <= num_levels) D = forced;
   if (forced < 0 && num_levels >= 10 - forced - 1) D = forced;

@@ -3,24 +3,27 @@ of the benchmarked configuration at its full size.
 
 `dpf_amd_expand_and_correct` picks the kernel from the launch size
 (kernels_capi.cc): KExpand<8> (register DFS of depth 8 per thread) once a
-launch covers >= 2^25 tree leaves, the cooperative KExpandCoop (2^10 or 2^11
-leaves per block) below that when the tree has >= 11 levels, KExpand<D> with
-D = 4 / 2 / 1 on smaller trees.  These tests
+launch covers >= 2^25 tree leaves, KExpand<4> from 2^22, the cooperative
+KExpandCoop (2^10 leaves per block below 2^19 tree leaves, 2^11 from there)
+below that when the tree has >= 11 levels, KExpand<D> with D = 4 / 2 / 1 on
+smaller trees.  These tests
   * force D in {1, 2, 4, 8} and each KExpandCoop variant
     (dpf_amd_set_expand_depth) on small domains and compare every output of
     every value type with the oracle;
-  * run the automatic choice at sizes where it picks KExpandCoop (2^11-2^24
-    tree leaves) and KExpand<8> (2^25) and compare every output with the
-    oracle;
+  * run the automatic choice at sizes where it picks KExpandCoop (2^11-2^21
+    tree leaves), KExpand<4> (2^24) and KExpand<8> (2^25) and compare every
+    output with the oracle;
   * run the c5 bench configuration itself (log_domain_size 32,
     Tuple<uint32, IntModN<uint64, 2^64-59>>, the KExpand<8, EmitU32ModN64>
-    launch the bench times) for both parties: the share sum over all 2^32
-    leaves is checked on the device (beta at alpha, 0 elsewhere — the
-    reference's own full-domain property, distributed_point_function_test.cc:
-    652-696), sampled 2^20-leaf subtrees are compared bit-exactly with the
-    oracle, leaf-range slices above 2^31 equal the matching part of the full
-    launch, and bench.py's 8-rank subtree split (sharding.block_range), run
-    rank by rank on this GPU, reproduces the 1-rank output.
+    launch the bench times) for both parties: every one of the 2^32 leaves
+    of both parties is compared with the oracle through per-2^20-leaf-subtree
+    SHA-256 digests (tests/golden/c5_subtree_digests.json); the share sum
+    over all leaves (beta at alpha, 0 elsewhere — the reference's own
+    full-domain property, distributed_point_function_test.cc:652-696) checks
+    the alpha path; leaf-range slices above 2^31 equal the matching part of
+    the full launch, and bench.py's 8-rank subtree split
+    (sharding.block_range), run rank by rank on this GPU, reproduces the
+    1-rank output.
 """
 import random
 
@@ -147,12 +150,12 @@ def test_cooperative_kernel_leaf_ranges(K, cuda, coop):
             _assert_host_layout_equals_words(C5, got, want[lo:hi], "[%d, %d)" % (lo, hi))
 
 
-@pytest.mark.parametrize("ld", [12, 20, 21, 25])
+@pytest.mark.parametrize("ld", [12, 20, 21, 22, 25])
 def test_automatic_cooperative_launch_matches_oracle(K, cuda, ld):
-    """Sizes where the automatic choice runs KExpandCoop: uint64 at
-    log_domain_size 12 (2^11 tree leaves, two blocks) and 20 (c1: 2^19 tree
-    leaves) -> 1024-leaf blocks; 21 and 25 (2^20, 2^24 tree leaves) ->
-    2048-leaf blocks; every output against the oracle."""
+    """The automatic choice around the cooperative kernel: uint64 at
+    log_domain_size 12 (2^11 tree leaves, two blocks) -> 1024-leaf blocks;
+    20 (c1: 2^19 tree leaves), 21 and 22 (2^20, 2^21) -> 2048-leaf blocks;
+    25 (2^24) -> KExpand<4>; every output against the oracle."""
     import torch
     spec = ("int", 64)
     d, k0, k1, alpha, beta = _keys(spec, ld, seed=19)

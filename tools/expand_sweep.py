@@ -40,7 +40,7 @@ if mode == "single":
         cepb = 1 << (ld - L)
         out = torch.empty((1 << L) * cepb * desc.out_stride, dtype=torch.uint8, device=dev)
         res = {}
-        for D in (0, 2, 4, 8, -1, -2):
+        for D in (2, 4, 8, -1, -2, 0):  # the automatic choice last (warm clocks)
             def step():
                 kernels.expand_and_correct(kd["seed"], kd["cb"], L, kd["cw"], kd["ccl"], kd["ccr"],
                                            desc, kd["corr"], kd["party"], cepb, 0, 1 << L, out)
@@ -64,7 +64,7 @@ else:
         parties = [k["party"] for k in kd]
         out = torch.empty(q * leaves * 16, dtype=torch.uint8, device=dev)
         res = {}
-        for D in (0, 2, 4, 8, -1, -2):
+        for D in (2, 4, 8, -1, -2, 0):  # the automatic choice last (warm clocks)
             def step():
                 kernels.expand_and_correct_batched(seeds, cbs, L, cws, ccl, ccr, desc, corr,
                                                    parties, 1, 0, leaves, out)
