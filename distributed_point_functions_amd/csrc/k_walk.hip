@@ -431,6 +431,70 @@ __global__ __launch_bounds__(kDcfBlockOf<BN>, kDcfWavesOf<BN>) void KDcfEvaluate
   }
 }
 
+// KDcfEvaluate for a single integer / XorWrapper scalar of B bytes (uint64
+// DCFs, the reference's BM_EvaluateDcf shape): the element, its correction,
+// the negation and the sum stay in registers (U = uint64 up to 8 bytes,
+// u128 for 16) — the generic kernel stages each level's element through a
+// byte buffer and indexes its correction and accumulator arrays at run
+// time, which lands them in scratch (1 KiB per lane).
+template <bool XOR, int B>
+__global__ __launch_bounds__(kDcfBlockOf<1>, kDcfWavesOf<1>) void KDcfEvaluateDirect(DcfArgs a,
+                                                                                    VtDev vt) {
+  using U = typename std::conditional<(B > 8), u128, uint64_t>::type;
+  __shared__ uint32_t tab[kTabWords];
+  FillTables(tab);
+  __syncthreads();
+  const Lds L = MakeLds(tab);
+  const int64_t T = (int64_t)gridDim.x * blockDim.x;
+  const int per_elem = vt.epb;
+  const int H = a.log_domain;
+  const U mask = B >= (int)sizeof(U) ? ~(U)0 : (((U)1 << (8 * B)) - 1);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += T) {
+    const uint4 s0 = a.seeds[i];
+    uint32_t x[4] = {s0.x, s0.y, s0.z, s0.w};
+    uint32_t t = a.cb[i];
+    const uint4 p = a.points[i];
+    const u128 pv = (u128)p.x | ((u128)p.y << 32) | ((u128)p.z << 64) | ((u128)p.w << 96);
+    const bool negate = a.party[i] == 1;
+    U acc = 0;
+    int level = 0;
+    for (int h = 0; h < H; ++h) {
+      const int stop = a.tree_of[h];
+      for (; level < stop; ++level) {
+        const uint32_t bit = PathBit(p, H - 1 - level);
+        const Cw cw = LoadCw(a.cw_seed, a.ccl, a.ccr, (int64_t)level * a.n + i);
+        WalkStep(x, t, bit, cw, DpfMasked<1>{{0u - bit}}, L);
+      }
+      if (PathBit(p, H - 1 - h) != 0) continue;
+      u128 W[1][1];
+      const uint32_t xs[1][4] = {{x[0], x[1], x[2], x[3]}};
+      HashSeeds<1, 1>(xs, W, L);
+      const int bbits = h - stop;
+      const int e = bbits > 0 ? (int)((pv >> (H - h)) & (((u128)1 << bbits) - 1)) : 0;
+      U v = (U)(W[0][0] >> (8 * B * e)) & mask;
+      const uint4 c = a.corrections[((int64_t)h * a.n + i) * per_elem + e];
+      const U corr =
+          (U)((u128)c.x | ((u128)c.y << 32) | ((u128)c.z << 64) | ((u128)c.w << 96)) & mask;
+      if (XOR) {
+        if (t) v ^= corr;
+        acc ^= v;  // XorWrapper: -v = v
+      } else {
+        if (t) v = (v + corr) & mask;
+        acc = (negate ? acc - v : acc + v) & mask;
+      }
+    }
+    char* out = a.out + i * (int64_t)vt.stride;
+    StoreScalar(out + vt.sc[0].out_off, B, (u128)acc);
+  }
+}
+
+template <bool XOR, int B>
+static void LaunchDcfDirect(hipStream_t st, const DcfArgs& a, const VtDev& vt) {
+  const int block = WalkBlock(a.n, kDcfBlockOf<1>);
+  const int grid = (int)std::min<int64_t>(DPF_DCF_MAX_GRID, (a.n + block - 1) / block);
+  hipLaunchKernelGGL((KDcfEvaluateDirect<XOR, B>), dim3(grid), dim3(block), 0, st, a, vt);
+}
+
 template <int BN>
 static void LaunchDcf(hipStream_t st, const DcfArgs& a, const VtDev& vt) {
   const int block = WalkBlock(a.n, kDcfBlockOf<BN>);
@@ -439,6 +503,32 @@ static void LaunchDcf(hipStream_t st, const DcfArgs& a, const VtDev& vt) {
 }
 
 int LaunchDcfEvaluate(int bn, hipStream_t st, const DcfArgs& a, const VtDev& vt) {
+  const ScalarDev& s0 = vt.sc[0];
+  const bool one_direct = vt.direct && vt.ns == 1 && bn == 1 && s0.in_off == 0 &&
+                          vt.esz == s0.bytes &&
+                          (s0.kind == DPF_AMD_KIND_INTEGER || s0.kind == DPF_AMD_KIND_XOR_WRAPPER);
+  if (one_direct && DcfDirectEnabled()) {
+    const bool x = s0.kind == DPF_AMD_KIND_XOR_WRAPPER;
+    switch (s0.bytes) {
+      case 1:
+        x ? LaunchDcfDirect<true, 1>(st, a, vt) : LaunchDcfDirect<false, 1>(st, a, vt);
+        return LaunchCheck("dcf kernel launch");
+      case 2:
+        x ? LaunchDcfDirect<true, 2>(st, a, vt) : LaunchDcfDirect<false, 2>(st, a, vt);
+        return LaunchCheck("dcf kernel launch");
+      case 4:
+        x ? LaunchDcfDirect<true, 4>(st, a, vt) : LaunchDcfDirect<false, 4>(st, a, vt);
+        return LaunchCheck("dcf kernel launch");
+      case 8:
+        x ? LaunchDcfDirect<true, 8>(st, a, vt) : LaunchDcfDirect<false, 8>(st, a, vt);
+        return LaunchCheck("dcf kernel launch");
+      case 16:
+        x ? LaunchDcfDirect<true, 16>(st, a, vt) : LaunchDcfDirect<false, 16>(st, a, vt);
+        return LaunchCheck("dcf kernel launch");
+      default:
+        break;
+    }
+  }
   switch (bn) {
     case 1:
       LaunchDcf<1>(st, a, vt);

@@ -180,6 +180,9 @@ int LaunchEvaluatePoints(int bn, int64_t n, hipStream_t st, const PointsArgs& a,
                          const VtDev& vt);
 // The calling thread's point-walk kernel choice (dpf_amd_set_walk_mode).
 int WalkMode();
+// Whether this thread's DCF launches may use the single-scalar kernel
+// (dpf_amd_set_dcf_kernel).
+bool DcfDirectEnabled();
 int LaunchDcfEvaluate(int bn, hipStream_t st, const DcfArgs& a, const VtDev& vt);
 int LaunchAesMmo(int grid, hipStream_t st, const uint4* in, uint4* out, int64_t n,
                  const KeyPair& kp);

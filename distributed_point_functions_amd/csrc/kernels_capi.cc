@@ -25,6 +25,7 @@ namespace {
 // changes what another thread's launches pick.
 thread_local int t_expand_depth = 0;  // dpf_amd_set_expand_depth
 thread_local int t_walk_mode = 0;     // dpf_amd_set_walk_mode
+thread_local int t_dcf_generic = 0;   // dpf_amd_set_dcf_kernel
 // dpf_amd_set_scan_m4; the process default comes from DPF_AMD_SCAN_M4 (A/B runs)
 const int kScanM4Default = [] {
   const char* e = std::getenv("DPF_AMD_SCAN_M4");
@@ -117,6 +118,7 @@ int LaunchExpandForType(int D, int grid, hipStream_t st, const ExpandArgs& a,
 }  // namespace
 
 int WalkMode() { return t_walk_mode; }
+bool DcfDirectEnabled() { return t_dcf_generic == 0; }
 
 int MakeVtDev(const dpf_amd_value_type& vt, const uint64_t* correction, int party,
               int cepb, VtDev* out) {
@@ -368,6 +370,13 @@ int dpf_amd_set_expand_depth(int depth) {
     return -3;
   const int old = t_expand_depth;
   t_expand_depth = depth;
+  return old;
+}
+
+int dpf_amd_set_dcf_kernel(int mode) {
+  if (mode < 0 || mode > 1) return -2;
+  const int old = t_dcf_generic;
+  t_dcf_generic = mode;
   return old;
 }
 

@@ -180,6 +180,24 @@ class forced_walk_mode:
         _lib.lib().dpf_amd_set_walk_mode(self.prev)
 
 
+class forced_dcf_kernel:
+    """Context manager selecting this thread's DCF kernel
+    (dpf_amd_set_dcf_kernel: 0 automatic, 1 generic)."""
+
+    def __init__(self, mode: int):
+        self.mode = mode
+
+    def __enter__(self):
+        prev = _lib.lib().dpf_amd_set_dcf_kernel(self.mode)
+        if prev < 0:
+            raise ValueError("dcf kernel mode must be 0 or 1")
+        self.prev = prev
+        return self
+
+    def __exit__(self, *exc):
+        _lib.lib().dpf_amd_set_dcf_kernel(self.prev)
+
+
 def evaluate_points(seeds, control_bits, paths, paths_rightshift, num_levels,
                     cw_seeds, ccl, ccr, desc, block_index=None, party=None,
                     party_all: int = 0, value_corrections=None,

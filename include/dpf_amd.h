@@ -180,6 +180,12 @@ int dpf_amd_set_scan_m4(int mode);
  * (unchanged). */
 int dpf_amd_set_walk_mode(int mode);
 
+/* Test hook: the calling thread's DCF BatchEvaluate kernel.  0 = automatic
+ * (a single integer / XorWrapper scalar runs the register-only kernel),
+ * 1 = the generic kernel for every value type.  Returns the previous
+ * setting, or -2 for an invalid mode (unchanged). */
+int dpf_amd_set_dcf_kernel(int mode);
+
 /* Fused single-path evaluation: EvaluateSeeds from the given seeds along
  * `paths` (one AES per level, per-lane key select) + HashExpandedSeeds +
  * correction of element block_index[i] (EvaluateAtImpl h:1013-1063 and the

@@ -48,7 +48,7 @@ def _oracle_keys(spec, n, alpha, beta, seeds):
     """The oracle's incremental DPF with the DCF's levels and betas."""
     od = po.Dpf([(i, spec, 0) for i in range(n)])
     vt = V.from_spec(spec)
-    zero = vt.zero()
+    zero = vt.zero() if spec[0] != "xor" else beta  # SetToZero skips XorWrapper
     betas = [beta if (alpha >> (n - 1 - i)) & 1 else zero for i in range(n)]
     return od, od.generate_keys(alpha >> 1, betas, seeds=seeds)
 
@@ -137,10 +137,16 @@ def test_gen_eval_every_point(cuda, spec, n):
 @pytest.mark.gpu
 @pytest.mark.parametrize("spec,n", REF_TYPES[2:] + [(("int", 64), 64),
                                                      (("intmodn", 64, 18446744073709551557), 20),
-                                                     (("tuple", [("int", 16), ("int", 8)]), 12)],
+                                                     (("tuple", [("int", 16), ("int", 8)]), 12),
+                                                     (("int", 8), 7), (("int", 16), 11),
+                                                     (("xor", 64), 9), (("xor", 128), 33)],
                          ids=lambda x: repr(x))
-def test_batch_evaluate_matches_oracle(cuda, spec, n):
-    """Mixed keys and parties in one batch == the oracle composition."""
+@pytest.mark.parametrize("kernel", [0, 1], ids=["auto", "generic"])
+def test_batch_evaluate_matches_oracle(cuda, spec, n, kernel):
+    """Mixed keys and parties in one batch == the oracle composition, with
+    the automatic kernel (single integer / XorWrapper scalars run the
+    register-only KDcfEvaluateDirect) and forced to the generic one."""
+    from distributed_point_functions_amd import kernels as K
     rng = random.Random(n * 13 + len(repr(spec)))
     dcf = _dcf(spec, n)
     beta = _beta42(spec)
@@ -155,7 +161,8 @@ def test_batch_evaluate_matches_oracle(cuda, spec, n):
                 keys.append(k)
                 pts.append(x)
                 want.append(_oracle_dcf(od, o, n, x, spec))
-    got = dcf.batch_evaluate(keys, pts)
+    with K.forced_dcf_kernel(kernel):
+        got = dcf.batch_evaluate(keys, pts)
     assert got == want
 
 

@@ -404,10 +404,19 @@ def dcf(dev, reps):
             dptr(d_ccl), dptr(d_ccr), ctypes.byref(desc), dptr(d_corr), dptr(out),
             stream_ptr()))
     t_k = ev_time(run, reps)
+    fused = out.clone()
+    with kernels.forced_dcf_kernel(1):  # the generic kernel, for the record
+        t_g = ev_time(run, reps)
+    same = bool(torch.equal(out, fused))
+    # algorithmic AES: tree levels + one value hash per 0 bit of the point
+    zeros = sum(bin(int(x) ^ ((1 << H) - 1)).count("1") for x in pts[:4096, 0]) / 4096
+    aes = n * (L + zeros)
     return {"config": "dcf", "workload": "DCF BatchEvaluate log_domain=32 uint64",
             "api_keys": nkeys, "api_ms": t_api * 1e3,
             "kernel_evaluations": n, "kernel_ms": t_k * 1e3,
-            "kernel_evaluations_per_s": n / t_k, "correct": bool(ok)}
+            "kernel_evaluations_per_s": n / t_k, "generic_kernel_ms": t_g * 1e3,
+            "kernels_equal": same, "aes_per_evaluation": aes / n,
+            "lds_frac": aes * 160 / t_k / LDS_PEAK_LOOKUPS, "correct": bool(ok)}
 
 
 def cuckoo(dev, reps):
