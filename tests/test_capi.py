@@ -74,3 +74,28 @@ def test_kernel_choice_hooks_are_per_thread():
     assert seen["scan"] != 1 or os.environ.get("DPF_AMD_SCAN_M4") == "1"
     assert L.dpf_amd_set_expand_depth(0) == 4
     assert L.dpf_amd_set_scan_m4(-1) == 1
+
+
+def test_walk_and_dcf_kernel_hooks_validate_and_are_per_thread():
+    """dpf_amd_set_walk_mode (0 / 1 / 2) and dpf_amd_set_dcf_kernel (0 / 1):
+    invalid values are refused unchanged, and another thread keeps its own
+    setting."""
+    import threading
+    from distributed_point_functions_amd import _lib
+    L = _lib.lib()
+    assert L.dpf_amd_set_walk_mode(3) == -2
+    assert L.dpf_amd_set_dcf_kernel(2) == -2
+    assert L.dpf_amd_set_walk_mode(1) == 0
+    assert L.dpf_amd_set_dcf_kernel(1) == 0
+    seen = {}
+
+    def other():
+        seen["walk"] = L.dpf_amd_set_walk_mode(2)
+        seen["dcf"] = L.dpf_amd_set_dcf_kernel(0)
+
+    t = threading.Thread(target=other)
+    t.start()
+    t.join()
+    assert seen == {"walk": 0, "dcf": 0}
+    assert L.dpf_amd_set_walk_mode(0) == 1
+    assert L.dpf_amd_set_dcf_kernel(0) == 1
