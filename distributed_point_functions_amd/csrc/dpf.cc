@@ -1614,12 +1614,28 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
   hipStream_t s = ThreadStream();
   trace.Mark("validate");
 
+  // Tree indices and element indices of the points (h:1013-1019): for one
+  // element per block the points are the tree indices themselves; otherwise
+  // they go to per-thread scratch (fresh 16-byte-per-point vectors cost more
+  // in page faults than the loop that fills them).
   const int bbits = log_domain_size - m.tree_level;
-  std::vector<uint128> tree(n);
-  std::vector<uint8_t> bidx(n, 0);
-  for (int64_t i = 0; i < n; ++i) {
-    tree[i] = m.epb > 1 ? (evaluation_points[i] >> bbits) : evaluation_points[i];
-    if (m.epb > 1) bidx[i] = static_cast<uint8_t>(evaluation_points[i] & ((uint128{1} << bbits) - 1));
+  struct PointScratch {
+    std::vector<uint128> tree;
+    std::vector<uint8_t> bidx;
+  };
+  PointScratch& ps = dpf_internal_host::ThreadRecycled<PointScratch>::Get();
+  const uint128* tree = evaluation_points.data();
+  const uint8_t* bidx = nullptr;
+  if (m.epb > 1) {
+    if (static_cast<int64_t>(ps.tree.size()) < n) ps.tree.resize(n);
+    if (static_cast<int64_t>(ps.bidx.size()) < n) ps.bidx.resize(n);
+    const uint128 bmask = (uint128{1} << bbits) - 1;
+    for (int64_t i = 0; i < n; ++i) {
+      ps.tree[i] = evaluation_points[i] >> bbits;
+      ps.bidx[i] = static_cast<uint8_t>(evaluation_points[i] & bmask);
+    }
+    tree = ps.tree.data();
+    bidx = ps.bidx.data();
   }
   if (ctx == nullptr) {
     // The common call (one EvaluateAt per key): every input in one pinned
@@ -1631,7 +1647,7 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
     const int levels = m.tree_level;
     CwArrays cw = KeyCws(key, 0, levels);
     using Part = UploadRing::HostPart;
-    const Part parts[6] = {{tree.data(), size_t(16) * n},
+    const Part parts[6] = {{tree, size_t(16) * n},
                            {&seed, 16},
                            {cw.seeds.data(), size_t(16) * levels},
                            {cw.ccl.data(), size_t(levels)},
@@ -1646,7 +1662,7 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
     DPF_RETURN_IF_ERROR(buf.Alloc(out_off + size_t(n) * vt.out_stride, s));
     char* d = buf.as<char>();
     DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 6, in_bytes, off, s));
-    if (m.epb > 1) DPF_RETURN_IF_ERROR(ThreadUploadRing().Copy(d + bi_off, bidx.data(), n, s));
+    if (m.epb > 1) DPF_RETURN_IF_ERROR(ThreadUploadRing().Copy(d + bi_off, bidx, n, s));
     DPF_RETURN_IF_ERROR(ClearPadding(vt, d + out_off, n * vt.out_stride, s));
     trace.Mark("alloc+upload");
     DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_points_batched(
@@ -1665,14 +1681,14 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
   DeviceBuffer pe, paths, bi, cws, ccl, ccr, dout;
   void* seeds = nullptr;
   uint8_t* cbs = nullptr;
-  DPF_RETURN_IF_ERROR(ComputePartialEvaluations(st, Span<const uint128>(tree.data(), n),
+  DPF_RETURN_IF_ERROR(ComputePartialEvaluations(st, Span<const uint128>(tree, n),
                                                 hierarchy_level, true, *ctx, s, &pe, &seeds,
                                                 &cbs));
   const int start_level = m.tree_level;
   const int levels = m.tree_level - start_level;
   CwArrays cw = KeyCws(key, start_level, m.tree_level);
-  DPF_RETURN_IF_ERROR(paths.Upload(tree.data(), 16 * n, s));
-  DPF_RETURN_IF_ERROR(bi.Upload(bidx.data(), n, s));
+  DPF_RETURN_IF_ERROR(paths.Upload(tree, 16 * n, s));
+  if (bidx) DPF_RETURN_IF_ERROR(bi.Upload(bidx, n, s));
   DPF_RETURN_IF_ERROR(cws.Upload(cw.seeds.data(), 16 * levels, s));
   DPF_RETURN_IF_ERROR(ccl.Upload(cw.ccl.data(), levels, s));
   DPF_RETURN_IF_ERROR(ccr.Upload(cw.ccr.data(), levels, s));
@@ -1680,8 +1696,9 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
   DPF_RETURN_IF_ERROR(ClearPadding(vt, dout.get(), n * vt.out_stride, s));
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_points(
       n, seeds, cbs, paths.get(), 0, levels, levels, cws.get(),
-      ccl.as<uint8_t>(), ccr.as<uint8_t>(), &vt, bi.as<uint8_t>(), nullptr, key.party(), nullptr,
-      reinterpret_cast<const uint64_t*>(corr.data()), dout.get(), nullptr, nullptr, s)));
+      ccl.as<uint8_t>(), ccr.as<uint8_t>(), &vt, bidx ? bi.as<uint8_t>() : nullptr, nullptr,
+      key.party(), nullptr, reinterpret_cast<const uint64_t*>(corr.data()), dout.get(), nullptr,
+      nullptr, s)));
   DPF_RETURN_IF_ERROR(CopyToHostSync(out, dout.get(), n * vt.out_stride, s));
   if (ctx) ctx->set_previous_hierarchy_level(hierarchy_level);
   return OkStatus();

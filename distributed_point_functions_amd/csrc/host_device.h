@@ -261,6 +261,16 @@ class HostPool {
   uint64_t gen_ = 0;
 };
 
+// Largest D2H copy into pageable memory left to the runtime's own path
+// (DPF_AMD_D2H_DIRECT_KB, default 1024; A/B of the staging threshold).
+inline size_t D2HDirectMax() {
+  static const size_t v = [] {
+    const char* e = std::getenv("DPF_AMD_D2H_DIRECT_KB");
+    return (e ? std::strtoull(e, nullptr, 10) : 1024ull) << 10;
+  }();
+  return v;
+}
+
 // Device-to-host copy into pageable `dst`, complete on return.  A plain
 // hipMemcpy into pageable memory stages through the runtime's own small
 // pinned buffers one after the other; copies above 1 MiB here go through two
@@ -383,7 +393,7 @@ class H2DStaging {
 inline H2DStaging& ThreadH2DStaging() { return ThreadRecycled<H2DStaging>::Get(); }
 
 inline Status CopyToHostSync(void* dst, const void* src, size_t bytes, hipStream_t s) {
-  if (bytes <= (size_t{1} << 20)) {
+  if (bytes <= D2HDirectMax()) {
     DPF_RETURN_IF_ERROR(CopyToHost(dst, src, bytes, s));
     return HipStatus(hipStreamSynchronize(s), "sync");
   }
