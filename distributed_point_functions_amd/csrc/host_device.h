@@ -104,19 +104,22 @@ class DeviceGuard {
   bool set_ = false;
 };
 
-// The calling thread's stream on `device` (sharded databases and multi-GPU
-// expansions issue each device's work on its own stream from one thread).
+// The calling thread's stream number `index` on `device` (sharded
+// databases and multi-GPU expansions issue each device's work on its own
+// stream from one thread; pieces of work on one device that should overlap
+// take different indices).
 struct ThreadStreams {
-  std::map<int, hipStream_t> s;
+  std::map<std::pair<int, int>, hipStream_t> s;
 };
-inline hipStream_t ThreadStreamOn(int device) {
+inline hipStream_t ThreadStreamOn(int device, int index = 0) {
   ThreadStreams& h = ThreadRecycled<ThreadStreams>::Get();
-  auto it = h.s.find(device);
+  const std::pair<int, int> key(device, index);
+  auto it = h.s.find(key);
   if (it != h.s.end()) return it->second;
   DeviceGuard g(device);
   hipStream_t st = nullptr;
   if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
-  h.s[device] = st;
+  h.s[key] = st;
   return st;
 }
 

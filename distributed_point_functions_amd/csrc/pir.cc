@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <functional>
+#include <map>
 
 #include "dpf_amd/dense_dpf_pir_server.h"
 #include "host_aes.h"
@@ -268,35 +269,71 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductWithDevice(
   return r;
 }
 
+// Pieces per shard: DPF_AMD_PIR_SPLIT = k scans a shard as k 128-aligned row
+// ranges on k streams of its device, so one range's selection expansion can
+// run beside another's scan.  Measured on c4 (C++ HandleRequest, one box):
+// Q = 8 2.84 ms whole vs 3.01 in two pieces; Q = 64 6.43 vs 6.77 (two) and
+// 6.34 (four) — the scan's grid already fills the chip and each piece adds
+// its own tail and fold, so the default is one piece.
+int PiecesPerShard(int64_t rows) {
+  static const int forced = [] {
+    const char* e = std::getenv("DPF_AMD_PIR_SPLIT");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced > 1) return static_cast<int>(std::min<int64_t>(forced, std::max<int64_t>(1, rows / 128)));
+  return 1;
+}
+
 StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
     const FillSelectionsFn& fill, int num_queries) const {
   using dpf_internal_host::DeviceGuard;
   using dpf_internal_host::DevicePool;
   if (num_queries == 0) return std::vector<std::string>();
   if (max_value_size_ <= 0) return InvalidArgumentError("`max_value_size` must be positive");
-  const size_t G = shards_.size();
   const int64_t part_bytes = static_cast<int64_t>(num_queries) * stride_;
+  // Work pieces: each shard (or, with DPF_AMD_PIR_SPLIT, each of its
+  // 128-aligned row ranges) on a stream of its own — pieces on one device
+  // take consecutive stream indices, so shards that share a device overlap.
   struct Work {
+    Shard sh;
     hipStream_t s = nullptr;
     void* sel = nullptr;
     void* ws = nullptr;
     void* part = nullptr;
     hipEvent_t done = nullptr;
   };
-  std::vector<Work> w(G);
+  std::vector<Work> w;
+  {
+    std::map<int, int> next_index;
+    for (const Shard& sh : shards_) {
+      const int64_t rows = sh.row_end - sh.row_begin;
+      const int k = PiecesPerShard(rows);
+      const int64_t per = ((rows + k - 1) / k + 127) / 128 * 128;
+      for (int p = 0; p < k; ++p) {
+        const int64_t r0 = sh.row_begin + p * per;
+        const int64_t r1 = std::min(sh.row_end, r0 + per);
+        if (r1 <= r0 && p > 0) break;
+        Work x;
+        x.sh = Shard{sh.device, r0, r1,
+                     static_cast<char*>(sh.records) + (r0 - sh.row_begin) * stride_};
+        x.s = dpf_internal_host::ThreadStreamOn(sh.device, next_index[sh.device]++);
+        w.push_back(x);
+      }
+    }
+  }
+  const size_t G = w.size();
   dpf_internal_host::HostTrace trace("InnerProductSharded");
   const int dev0 = shards_[0].device;
-  hipStream_t s0 = dpf_internal_host::ThreadStreamOn(dev0);
+  hipStream_t s0 = w[0].s;
   void* gather = nullptr;
   void* folded = nullptr;
   std::vector<char> host(part_bytes);
   Status st = OkStatus();
-  // 1. every shard: its selection blocks, then its scan, on its own device
+  // 1. every piece: its selection blocks, then its scan, on its own stream
   for (size_t g = 0; g < G && st.ok(); ++g) {
-    const Shard& sh = shards_[g];
-    DeviceGuard dg(sh.device);
     Work& x = w[g];
-    x.s = dpf_internal_host::ThreadStreamOn(sh.device);
+    const Shard& sh = x.sh;
+    DeviceGuard dg(sh.device);
     if (x.s == nullptr) {
       st = InternalError("no stream on device " + std::to_string(sh.device));
       break;
@@ -320,7 +357,7 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
     }
   }
   trace.Mark("selections+scan_launch");
-  // 2. combine on the first shard's device: peer copies of the partials,
+  // 2. combine on the first shard's device: (peer) copies of the partials,
   // one XOR fold, one D2H
   const void* result = nullptr;
   if (st.ok()) {
@@ -334,11 +371,11 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
         char* dst = static_cast<char*>(gather) + g * part_bytes;
         st = HipStatus(hipStreamWaitEvent(s0, w[g].done, 0), "hipStreamWaitEvent");
         if (!st.ok()) break;
-        if (shards_[g].device == dev0)
+        if (w[g].sh.device == dev0)
           st = HipStatus(hipMemcpyAsync(dst, w[g].part, part_bytes, hipMemcpyDeviceToDevice, s0),
                          "partials copy");
         else
-          st = HipStatus(hipMemcpyPeerAsync(dst, dev0, w[g].part, shards_[g].device, part_bytes,
+          st = HipStatus(hipMemcpyPeerAsync(dst, dev0, w[g].part, w[g].sh.device, part_bytes,
                                             s0),
                          "partials peer copy");
       }
@@ -347,15 +384,14 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
       result = folded;
     }
     if (st.ok())
-      st = HipStatus(hipMemcpyAsync(host.data(), result, part_bytes, hipMemcpyDeviceToHost,
-                                    G == 1 ? w[0].s : s0),
+      st = HipStatus(hipMemcpyAsync(host.data(), result, part_bytes, hipMemcpyDeviceToHost, s0),
                      "d2h");
   }
   trace.Mark("combine_launch");
   // 3. drain every stream used, then return the buffers (no copy still reads them)
   for (size_t g = 0; g < G; ++g) {
     if (!w[g].s) continue;
-    DeviceGuard dg(shards_[g].device);
+    DeviceGuard dg(w[g].sh.device);
     Status sy = HipStatus(hipStreamSynchronize(w[g].s), "sync");
     if (st.ok()) st = sy;
   }
@@ -367,7 +403,7 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
     if (folded) DevicePool::Get().Free(folded, s0);
   }
   for (size_t g = 0; g < G; ++g) {
-    DeviceGuard dg(shards_[g].device);
+    DeviceGuard dg(w[g].sh.device);
     for (void* p : {w[g].sel, w[g].ws, w[g].part})
       if (p) DevicePool::Get().Free(p, w[g].s);
     if (w[g].done) (void)hipEventDestroy(w[g].done);
