@@ -563,10 +563,20 @@ int LaunchExpandCoop(hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
 }
 
 // D >= 0: KExpand with DFS depth D; D = -1 / -2: KExpandCoop with E = 0 / 1.
+// D = 6 is instantiated only for the PIR selection type (16-byte direct
+// elements), where large batched selection expansions use it.
+template <class Em>
+inline constexpr bool kHasDepth6 = false;
+template <>
+inline constexpr bool kHasDepth6<EmitDirect<16>> = true;
+
 template <class Em>
 int LaunchExpandAnyD(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
   if (D == -1) return LaunchExpandCoop<0, Em>(st, a, vt);
   if (D == -2) return LaunchExpandCoop<1, Em>(st, a, vt);
+  if constexpr (kHasDepth6<Em>) {
+    if (D == 6) return LaunchExpand<6, Em>(grid, st, a, vt);
+  }
   switch (D) {
     case 0:
       return LaunchExpand<0, Em>(grid, st, a, vt);

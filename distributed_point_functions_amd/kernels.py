@@ -135,7 +135,7 @@ class forced_expand_depth:
     def __enter__(self):
         prev = _lib.lib().dpf_amd_set_expand_depth(self.depth)
         if prev < -2:
-            raise ValueError("expand depth must be 0, 1, 2, 4, 8, -1 or -2")
+            raise ValueError("expand depth must be 0, 1, 2, 4, 6, 8, -1 or -2")
         self.prev = prev
         return self
 

@@ -97,9 +97,11 @@ def _assert_host_layout_equals_words(spec, got: np.ndarray, words: np.ndarray, w
 # Every DFS depth, every value type, whole domain vs oracle
 # ---------------------------------------------------------------------------
 
-@pytest.mark.parametrize("depth", [1, 2, 4, 8])
+@pytest.mark.parametrize("depth", [1, 2, 4, 6, 8])
 @pytest.mark.parametrize("spec", TYPES, ids=[repr(t) for t in TYPES])
 def test_forced_depth_matches_oracle(K, cuda, spec, depth):
+    """D = 6 exists for 16-byte direct types (the PIR selection); other
+    types run D = 8 for it."""
     d, k0, k1, alpha, beta = _keys(spec, 14, seed=depth)
     assert d.hierarchy_to_tree(0) >= depth
     with K.forced_expand_depth(depth):
@@ -376,7 +378,7 @@ def test_c5_eight_rank_split_reproduces_one_rank(K, cuda, c5_full):
         assert _chunked_equal(buf, full), world
 
 
-@pytest.mark.parametrize("variant", [0, 2, 4, 8, -1, -2])
+@pytest.mark.parametrize("variant", [0, 2, 4, 6, 8, -1, -2])
 @pytest.mark.parametrize("spec,ld", [(("xor", 128), 14), (("int", 64), 15), (("int", 32), 16),
                                      (("int", 8), 18), (C5, 13)])
 def test_batched_keys_match_oracle(K, cuda, spec, ld, variant):

@@ -64,7 +64,7 @@ else:
         parties = [k["party"] for k in kd]
         out = torch.empty(q * leaves * 16, dtype=torch.uint8, device=dev)
         res = {}
-        for D in (2, 4, 8, -1, -2, 0):  # the automatic choice last (warm clocks)
+        for D in (2, 4, 6, 8, -1, -2, 0):  # the automatic choice last (warm clocks)
             def step():
                 kernels.expand_and_correct_batched(seeds, cbs, L, cws, ccl, ccr, desc, corr,
                                                    parties, 1, 0, leaves, out)
