@@ -5,12 +5,18 @@
 // Checks mirror the reference's tests:
 //   distributed_point_function_test.cc:1015-1042 (full-domain share-sum),
 //   :1044-1079 (EvaluateAt share-sum), :652-696 (incremental),
-//   distributed_comparison_function_test.cc:106-133 (GenEval).
+//   distributed_comparison_function_test.cc:106-133 (GenEval),
+//   pir/dense_dpf_pir_server_test.cc (plain requests reconstruct records),
+//   here over a database sharded with Builder::SetDevices.
 // Exit status 0 = all checks passed.  Built and run by tests/test_cpp_api.py.
+#include <algorithm>
 #include <cstdio>
+#include <memory>
+#include <string>
 #include <set>
 #include <vector>
 
+#include "dpf_amd/dense_dpf_pir_server.h"
 #include "dpf_amd/distributed_comparison_function.h"
 #include "dpf_amd/distributed_point_function.h"
 
@@ -244,9 +250,134 @@ static int IncrementalManyPrefixes() {
   return 0;
 }
 
+// EvaluateAndApply over many points that share a few key objects (the
+// reference takes one key per point; callers pass the same key repeatedly):
+// every share pair sums to beta at alpha and to 0 elsewhere, per level.
+static int EvaluateAndApplyRepeatedKeys() {
+  std::vector<DpfParameters> ps(2);
+  ps[0].set_log_domain_size(10);
+  ps[1].set_log_domain_size(20);
+  for (auto& p : ps) p.mutable_value_type()->mutable_integer()->set_bitsize(32);
+  auto dpf = DistributedPointFunction::CreateIncremental(ps);
+  CHECK_OK(dpf);
+  const uint128 alphas[3] = {0x12345, 0xfffff, 0};
+  std::vector<std::pair<DpfKey, DpfKey>> pairs;
+  for (int k = 0; k < 3; ++k) {
+    auto kp = (*dpf)->GenerateKeysIncremental(alphas[k], std::vector<uint128>{7u + k, 100u + k});
+    CHECK_OK(kp);
+    pairs.push_back(*kp);
+  }
+  const int n = 3000;
+  std::vector<DpfKey> k0, k1;
+  std::vector<uint128> pts;
+  for (int i = 0; i < n; ++i) {
+    const int k = (i / 7) % 3;  // runs of one key, then switches
+    k0.push_back(pairs[k].first);
+    k1.push_back(pairs[k].second);
+    pts.push_back(i % 5 == 0 ? alphas[k] : uint128((i * 2654435761u) & 0xfffff));
+  }
+  std::vector<std::vector<uint32_t>> a, b;
+  auto sa = (*dpf)->EvaluateAndApply<uint32_t>(
+      Span<const DpfKey>(k0.data(), k0.size()), Span<const uint128>(pts.data(), pts.size()),
+      [&a](Span<const uint32_t> v) {
+        a.emplace_back(v.begin(), v.end());
+        return true;
+      });
+  auto sb = (*dpf)->EvaluateAndApply<uint32_t>(
+      Span<const DpfKey>(k1.data(), k1.size()), Span<const uint128>(pts.data(), pts.size()),
+      [&b](Span<const uint32_t> v) {
+        b.emplace_back(v.begin(), v.end());
+        return true;
+      });
+  CHECK(sa.ok() && sb.ok());
+  CHECK(a.size() == 2 && b.size() == 2);
+  if (a.size() != 2 || b.size() != 2) return 1;
+  for (int h = 0; h < 2; ++h) {
+    CHECK(a[h].size() == size_t(n) && b[h].size() == size_t(n));
+    const int shift = h == 0 ? 10 : 0;
+    for (int i = 0; i < n; ++i) {
+      const int k = (i / 7) % 3;
+      const bool hit = (pts[i] >> shift) == (alphas[k] >> shift);
+      const uint32_t want = hit ? (h == 0 ? 7u + k : 100u + k) : 0u;
+      if (uint32_t(a[h][i] + b[h][i]) != want) {
+        CHECK(uint32_t(a[h][i] + b[h][i]) == want);
+        return 1;
+      }
+    }
+  }
+  return 0;
+}
+
+// Two plain DenseDpfPirServers over the same records, one database on one
+// shard and one split into three shards with Builder::SetDevices (all on
+// device 0 here; the same code path peer-copies partials across GPUs): the
+// XOR of their responses is each requested record, zero padded to the
+// longest record (dense_dpf_pir_client.cc:124-161).
+static int PirShardedPlainRequests() {
+  const int64_t n = 1000;  // not a multiple of the 128-record block
+  std::vector<std::string> recs(n);
+  for (int64_t i = 0; i < n; ++i) {
+    recs[i].resize(1 + (i * 7) % 40);
+    for (size_t j = 0; j < recs[i].size(); ++j) recs[i][j] = char((i * 31 + j * 17 + 5) & 255);
+  }
+  size_t max_len = 0;
+  for (auto& r : recs) max_len = std::max(max_len, r.size());
+  PirConfig cfg;
+  cfg.mutable_dense_dpf_pir_config()->set_num_elements(n);
+  auto make = [&](std::vector<int> devices) -> std::unique_ptr<DenseDpfPirServer> {
+    DenseDpfPirDatabase::Builder b;
+    for (auto& r : recs) b.Insert(r);
+    if (!devices.empty()) b.SetDevices(devices);
+    auto db = b.Build();
+    if (!db.ok()) return nullptr;
+    auto s = DenseDpfPirServer::CreatePlain(cfg, std::move(*db));
+    return s.ok() ? std::move(*s) : nullptr;
+  };
+  auto s0 = make({});
+  auto s1 = make({0, 0, 0});
+  CHECK(s0 && s1);
+  if (!s0 || !s1) return 1;
+  // the client's DPF (dense_dpf_pir_client.cc:50-75): ceil(log2 n) levels,
+  // XorWrapper<uint128> values
+  DpfParameters cp;
+  cp.set_log_domain_size(10);
+  cp.mutable_value_type()->mutable_xor_wrapper()->set_bitsize(128);
+  auto client = DistributedPointFunction::Create(cp);
+  CHECK_OK(client);
+  const int64_t idx[] = {0, 127, 128, 517, 999, 517};
+  PirRequest r0, r1;
+  for (int64_t i : idx) {
+    auto kp = (*client)->GenerateKeys(uint128(i / 128),
+                                     XorWrapper<uint128>(uint128(1) << (i % 128)));
+    CHECK_OK(kp);
+    *r0.mutable_dpf_pir_request()->mutable_plain_request()->add_dpf_key() = kp->first;
+    *r1.mutable_dpf_pir_request()->mutable_plain_request()->add_dpf_key() = kp->second;
+  }
+  auto a = s0->HandleRequest(r0);
+  auto b = s1->HandleRequest(r1);
+  CHECK_OK(a);
+  CHECK_OK(b);
+  const auto& ma = a->dpf_pir_response();
+  const auto& mb = b->dpf_pir_response();
+  CHECK(ma.masked_response_size() == 6 && mb.masked_response_size() == 6);
+  if (ma.masked_response_size() != 6 || mb.masked_response_size() != 6) return 1;
+  for (int q = 0; q < 6; ++q) {
+    const std::string& x = ma.masked_response(q);
+    const std::string& y = mb.masked_response(q);
+    CHECK(x.size() == max_len && y.size() == max_len);
+    std::string want = recs[idx[q]];
+    want.resize(max_len, '\0');
+    std::string got(max_len, '\0');
+    for (size_t j = 0; j < max_len && j < x.size() && j < y.size(); ++j) got[j] = x[j] ^ y[j];
+    CHECK(got == want);
+  }
+  return 0;
+}
+
 int main() {
   if (FullDomainUint64() || IncrementalTuple() || DcfGenEval() || Registration() ||
-      EvaluateAndApplyStops() || IncrementalManyPrefixes())
+      EvaluateAndApplyStops() || IncrementalManyPrefixes() || EvaluateAndApplyRepeatedKeys() ||
+      PirShardedPlainRequests())
     return 2;
   if (failures) {
     std::fprintf(stderr, "%d check(s) failed\n", failures);
