@@ -328,7 +328,8 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
 // (256 B each); VALU: 11 + 2 + 64 XORs per lane.  Records past num_records
 // and slice dwords past the record read as zero, so they add nothing.
 //
-// Measured on MI355X, c4 (2^26 x 256 B), Q = 64 (masked scan: 15.0 ms):
+// Measured on MI355X, c4 (2^26 x 256 B), Q = 64 (masked scan: 15.0 ms; two
+// tables per step with XOR3 accumulators, ScanM4Tile2 below: 4.12 ms):
 // this kernel 4.50 ms with ds_write_addtid row stores, 4.79 ms with
 // ds_write2_b32 stores (7 address VGPRs).  Rejected: deeper register
 // prefetch (2 / 4 groups at 2 waves/SIMD: 5.29 / 5.54 ms), row reads in
@@ -451,6 +452,114 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
   }
 }
 
+// Two 4-record groups per step, each with its own table (tables A and B,
+// 4352 bytes apart), so every accumulator takes both selected rows in one
+// three-input XOR (gfx950 v_bitop3_b32): the VALU work per group halves
+// (64 accumulator XORs per 8 records instead of per 4) while the LDS work
+// stays 15 row stores + one row read per query per group.
+#ifndef DPF_SCAN_M4_DUAL
+#define DPF_SCAN_M4_DUAL 1
+#endif
+#ifndef DPF_SCAN_M4_DUAL_RB
+#define DPF_SCAN_M4_DUAL_RB 4  // row-pair reads in flight (8 VGPRs each)
+#endif
+__device__ __forceinline__ uint32_t Xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// Stores rows 1..15 of the table at M0 + `base` from the 4 record slices.
+#define DPF_M4_STORE_TABLE(base, x)                                                       \
+  do {                                                                                    \
+    const uint32_t x01 = x[0] ^ x[1], x02 = x[0] ^ x[2], x12 = x[1] ^ x[2];              \
+    const uint32_t x03 = x[0] ^ x[3], x13 = x[1] ^ x[3], x23 = x[2] ^ x[3];              \
+    const uint32_t x012 = Xor3(x[0], x[1], x[2]), x013 = Xor3(x[0], x[1], x[3]);         \
+    const uint32_t x023 = Xor3(x[0], x[2], x[3]), x123 = Xor3(x[1], x[2], x[3]);         \
+    const uint32_t x0123 = x01 ^ x23;                                                     \
+    asm volatile(                                                                         \
+        "s_nop 0\n\t"                                                                     \
+        "ds_write_addtid_b32 %0 offset:" #base "+272\n\t"                                 \
+        "ds_write_addtid_b32 %1 offset:" #base "+544\n\t"                                 \
+        "ds_write_addtid_b32 %2 offset:" #base "+816\n\t"                                 \
+        "ds_write_addtid_b32 %3 offset:" #base "+1088\n\t"                                \
+        "ds_write_addtid_b32 %4 offset:" #base "+1360\n\t"                                \
+        "ds_write_addtid_b32 %5 offset:" #base "+1632\n\t"                                \
+        "ds_write_addtid_b32 %6 offset:" #base "+1904\n\t"                                \
+        "ds_write_addtid_b32 %7 offset:" #base "+2176\n\t"                                \
+        "ds_write_addtid_b32 %8 offset:" #base "+2448\n\t"                                \
+        "ds_write_addtid_b32 %9 offset:" #base "+2720\n\t"                                \
+        "ds_write_addtid_b32 %10 offset:" #base "+2992\n\t"                               \
+        "ds_write_addtid_b32 %11 offset:" #base "+3264\n\t"                               \
+        "ds_write_addtid_b32 %12 offset:" #base "+3536\n\t"                               \
+        "ds_write_addtid_b32 %13 offset:" #base "+3808\n\t"                               \
+        "ds_write_addtid_b32 %14 offset:" #base "+4080"                                   \
+        :                                                                                 \
+        : "v"(x[0]), "v"(x[1]), "v"(x01), "v"(x[2]), "v"(x02), "v"(x12), "v"(x012),      \
+          "v"(x[3]), "v"(x03), "v"(x13), "v"(x013), "v"(x23), "v"(x023), "v"(x123),       \
+          "v"(x0123), "{m0}"((uint32_t)(uintptr_t)t)                                      \
+        : "memory");                                                                      \
+  } while (0)
+
+template <int P>
+__device__ __forceinline__ void ScanM4Tile2(const ScanArgs& a, int64_t tile, uint4 s,
+                                            uint32_t (&acc)[64 / P], uint32_t* t, int lane,
+                                            int cpart, bool col_ok, int dw_lo) {
+  constexpr int CPL = 16 / P;
+  constexpr int ROW = 17;
+  const int rec_dwords = a.C * 4;
+  const int64_t rec0 = tile << 7;
+  const bool full = rec0 + 128 <= a.num_records;
+  const uint32_t* base = reinterpret_cast<const uint32_t*>(a.db) + rec0 * rec_dwords + dw_lo;
+  const int64_t left = (a.num_records - rec0) * rec_dwords * 4 - dw_lo * 4;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)base, 0, full ? 0x7fffffff : (int)left, 0x00020000);
+  const int voff = col_ok ? lane * 4 : (int)0x80000000u;
+  const int rec_bytes = rec_dwords * 4;
+  auto load = [&](int r) -> uint32_t {
+    return __builtin_amdgcn_raw_buffer_load_b32(rsrc, col_ok ? voff + r * rec_bytes : voff, 0, 2);
+  };
+  // the next 8 records in flight; the last step re-reads the tile's first
+  // (cached) records rather than branching
+  uint32_t xq[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) xq[i] = load(i);
+#pragma unroll 1
+  for (int k = 0; k < 16; ++k) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t xa[4], xb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      xa[i] = xq[i];
+      xb[i] = xq[4 + i];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xq[i] = load((8 * (k + 1) + i) & 127);
+    DPF_M4_STORE_TABLE(0, xa);
+    DPF_M4_STORE_TABLE(4352, xb);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // groups 2k and 2k + 1: one selection byte, low nibble for table A
+    const uint32_t sb = (SelWord(s, k >> 2) >> (8 * (k & 3))) & 255;
+    const uint4* ra = reinterpret_cast<const uint4*>(t) + (sb & 15) * ROW + cpart * CPL;
+    const uint4* rb = reinterpret_cast<const uint4*>(t) + (16 + (sb >> 4)) * ROW + cpart * CPL;
+    constexpr int RB = CPL < DPF_SCAN_M4_DUAL_RB ? CPL : DPF_SCAN_M4_DUAL_RB;
+#pragma unroll
+    for (int c0 = 0; c0 < CPL; c0 += RB) {
+#pragma unroll
+      for (int c = c0; c < c0 + RB; ++c) {
+        const uint4 v = ra[c], w = rb[c];
+        acc[4 * c] = Xor3(acc[4 * c], v.x, w.x);
+        acc[4 * c + 1] = Xor3(acc[4 * c + 1], v.y, w.y);
+        acc[4 * c + 2] = Xor3(acc[4 * c + 2], v.z, w.z);
+        acc[4 * c + 3] = Xor3(acc[4 * c + 3], v.w, w.w);
+      }
+      if (RB < CPL) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
 #ifndef DPF_SCAN_M4_P1_WAVES
 #define DPF_SCAN_M4_P1_WAVES 4  // 100 VGPRs (5 waves: 4 spilled, Q = 64 4.31 vs 4.36 ms)
 #endif
@@ -460,7 +569,10 @@ void KPirScanM4(ScanArgs a) {
   constexpr int QW = 64 / P;        // queries per wave
   constexpr int CPL = 16 / P;       // 16-byte columns of the slice per lane
   constexpr int ROW = 17;           // uint4 per table row (272 B)
-  __shared__ uint4 tab[kScanM4Waves][16 * ROW];
+  // (P = 4 keeps one table: two would cap it at 4 waves/SIMD by LDS)
+  constexpr bool DUAL = DPF_SCAN_M4_DUAL && P <= 2;
+  constexpr int TABLES = DUAL ? 2 : 1;
+  __shared__ uint4 tab[kScanM4Waves][TABLES * 16 * ROW];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // qgroups = 2 (P = 1, 65-128 queries): the waves of a pair scan the same
@@ -477,6 +589,7 @@ void KPirScanM4(ScanArgs a) {
   const bool q_ok = q < a.nq;
   uint32_t* t = reinterpret_cast<uint32_t*>(tab[wave]);
   t[lane] = 0u;  // row 0 (no record selected) stays zero
+  if (TABLES == 2) t[16 * ROW * 4 + lane] = 0u;
   uint32_t acc[4 * CPL];
 #pragma unroll
   for (int i = 0; i < 4 * CPL; ++i) acc[i] = 0u;
@@ -484,7 +597,10 @@ void KPirScanM4(ScanArgs a) {
   for (int64_t tile = part; tile < tiles; tile += a.parts) {
     const uint4 s = q_ok ? a.sel[(int64_t)(a.q0 + q) * a.sel_blocks + tile]
                          : make_uint4(0, 0, 0, 0);
-    ScanM4Tile<P>(a, tile, s, acc, t, lane, cpart, col_ok, dw_lo);
+    if (DUAL)
+      ScanM4Tile2<P>(a, tile, s, acc, t, lane, cpart, col_ok, dw_lo);
+    else
+      ScanM4Tile<P>(a, tile, s, acc, t, lane, cpart, col_ok, dw_lo);
   }
   if (!q_ok) return;
   // this lane's columns [cpart * CPL, +CPL) of the slice, clipped to the record
