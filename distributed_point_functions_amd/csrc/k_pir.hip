@@ -614,6 +614,115 @@ void KPirScanM4(ScanArgs a) {
   }
 }
 
+// 65-128 queries, one wave pair per block sharing its tables: per step of 8
+// records wave w loads records 4w..4w+3 and builds table w (A or B) only,
+// one barrier publishes both, and each wave reads rows from both for its 64
+// queries.  Tables are double-buffered (step parity), so a wave overwrites a
+// buffer only after passing the next step's barrier, which its partner
+// reaches after finishing its reads of that buffer.  Against two private
+// table pairs this halves the row stores and the record loads per step.
+#ifndef DPF_SCAN_M4_SHARED
+#define DPF_SCAN_M4_SHARED 1
+#endif
+#ifndef DPF_SCAN_M4_PAIR_RB
+#define DPF_SCAN_M4_PAIR_RB 4  // row pairs in flight (118 VGPRs; 2: 102, Q = 100 6.11 vs 6.03 ms)
+#endif
+#ifndef DPF_SCAN_M4_PAIR_WAVES
+#define DPF_SCAN_M4_PAIR_WAVES 4
+#endif
+constexpr int kScanM4PairBlock = 128;
+
+__device__ __forceinline__ void ScanM4PairStep(const uint32_t (&x)[4], uint32_t sb, int buf,
+                                               uint32_t* t0, const uint4* tab0,
+                                               uint32_t (&acc)[64]) {
+  constexpr int ROW = 17;
+  // this wave's table in buffer `buf` (M0 = its base; buffer 1 is 8704 B on)
+  uint32_t* t = t0 + buf * (2 * 16 * ROW * 4);
+  DPF_M4_STORE_TABLE(0, x);
+  // LDS-only barrier: the tables are published, the next step's record loads
+  // stay in flight (__syncthreads would also wait for them, vmcnt(0))
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  const uint4* ra = tab0 + (2 * buf) * 16 * ROW + (sb & 15) * ROW;
+  const uint4* rb = tab0 + (2 * buf + 1) * 16 * ROW + (sb >> 4) * ROW;
+  constexpr int RB = DPF_SCAN_M4_PAIR_RB;
+#pragma unroll
+  for (int c0 = 0; c0 < 16; c0 += RB) {
+#pragma unroll
+    for (int c = c0; c < c0 + RB; ++c) {
+      const uint4 v = ra[c], w = rb[c];
+      acc[4 * c] = Xor3(acc[4 * c], v.x, w.x);
+      acc[4 * c + 1] = Xor3(acc[4 * c + 1], v.y, w.y);
+      acc[4 * c + 2] = Xor3(acc[4 * c + 2], v.z, w.z);
+      acc[4 * c + 3] = Xor3(acc[4 * c + 3], v.w, w.w);
+    }
+    if (RB < 16) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__global__ __launch_bounds__(kScanM4PairBlock, DPF_SCAN_M4_PAIR_WAVES)
+void KPirScanM4Pair(ScanArgs a) {
+  constexpr int ROW = 17;
+  // [buffer][table A/B][row]: wave w writes table w of each buffer
+  __shared__ uint4 tab[2][2][16 * ROW];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t part = blockIdx.x;  // block-uniform: both waves take the barriers
+  const int q = wave * 64 + lane;
+  const int dw_lo = blockIdx.y * 64;
+  const int width = min(64, a.C * 4 - dw_lo);
+  const bool col_ok = lane < width;
+  const bool q_ok = q < a.nq;
+  uint32_t* t = reinterpret_cast<uint32_t*>(tab[0][wave]);
+  const uint4* tab0 = &tab[0][0][0];
+  t[lane] = 0u;                  // row 0 of this wave's table, buffer 0
+  t[2 * 16 * ROW * 4 + lane] = 0u;  // and buffer 1
+  uint32_t acc[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) acc[i] = 0u;
+  const int64_t tiles = (a.num_records + 127) >> 7;
+  const int rec_dwords = a.C * 4;
+  const int rec_bytes = rec_dwords * 4;
+  for (int64_t tile = part; tile < tiles; tile += a.parts) {
+    const uint4 s = q_ok ? a.sel[(int64_t)(a.q0 + q) * a.sel_blocks + tile]
+                         : make_uint4(0, 0, 0, 0);
+    const int64_t rec0 = tile << 7;
+    const bool full = rec0 + 128 <= a.num_records;
+    const uint32_t* base =
+        reinterpret_cast<const uint32_t*>(a.db) + rec0 * rec_dwords + dw_lo;
+    const int64_t left = (a.num_records - rec0) * rec_dwords * 4 - dw_lo * 4;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)base, 0, full ? 0x7fffffff : (int)left, 0x00020000);
+    const int voff = col_ok ? lane * 4 : (int)0x80000000u;
+    auto load = [&](int r) -> uint32_t {
+      return __builtin_amdgcn_raw_buffer_load_b32(rsrc, col_ok ? voff + r * rec_bytes : voff, 0,
+                                                  2);
+    };
+    // this wave's 4 records of the next step in flight
+    uint32_t xq[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xq[i] = load(4 * wave + i);
+#pragma unroll 1
+    for (int k = 0; k < 16; ++k) {
+      uint32_t x[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        x[i] = xq[i];
+        xq[i] = load((8 * (k + 1) + 4 * wave + i) & 127);
+      }
+      ScanM4PairStep(x, (SelWord(s, k >> 2) >> (8 * (k & 3))) & 255, k & 1, t, tab0, acc);
+    }
+  }
+  if (!q_ok) return;
+  uint4* out = a.partials + (part * a.total_q + a.q0 + q) * a.C + blockIdx.y * 16;
+  const int chunks = (width + 3) / 4;
+#pragma unroll
+  for (int c = 0; c < 16; ++c)
+    if (c < chunks)
+      out[c] = make_uint4(acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]);
+}
+
 #ifndef DPF_SCAN_M4_PAIRS
 #define DPF_SCAN_M4_PAIRS 1  // wave pairs for 65-128 queries (else 64 per pass)
 #endif
@@ -627,7 +736,9 @@ int LaunchPirScanM4(int nq, int parts, int slices, hipStream_t st, const ScanArg
   a.qgroups = nq > 64 ? 2 : 1;
   const int per_block = kScanM4Waves / a.qgroups;
   const dim3 g((parts + per_block - 1) / per_block, slices);
-  if (P == 1)
+  if (DPF_SCAN_M4_SHARED && a.qgroups == 2) {
+    hipLaunchKernelGGL(KPirScanM4Pair, dim3(parts, slices), dim3(kScanM4PairBlock), 0, st, a);
+  } else if (P == 1)
     hipLaunchKernelGGL((KPirScanM4<1>), g, dim3(kScanM4Block), 0, st, a);
   else if (P == 2)
     hipLaunchKernelGGL((KPirScanM4<2>), g, dim3(kScanM4Block), 0, st, a);
