@@ -426,6 +426,36 @@ int LaunchExpand(int, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
 #define DPF_COOP_WAVES 8  // 2 blocks per CU (72 KiB LDS each)
 #endif
 constexpr int kCoopBlock = DPF_COOP_BLOCK;
+#ifndef DPF_COOP_QUAD_BFS
+#define DPF_COOP_QUAD_BFS 0  // breadth-first levels run as quad steps (0-2)
+#endif
+static_assert(DPF_COOP_QUAD_BFS >= 0 && DPF_COOP_QUAD_BFS <= 2, "quad BFS levels: 0-2");
+
+// Phase timestamps of KExpandCoop (diagnostic builds only: tools/coop_trace.py
+// builds one translation unit with DPF_COOP_TRACE=1): per block, thread 0's
+// s_memrealtime (100 MHz) at entry, after the tables, after the walk, after
+// the BFS and at the end.
+#if DPF_COOP_TRACE
+__device__ uint64_t g_coop_trace[4096 * 8];
+#define DPF_COOP_MARK(i)                                                      \
+  do {                                                                        \
+    if (DPF_COOP_TRACE_SYNC) __syncthreads();                                 \
+    if (threadIdx.x == 0 && blockIdx.x < 4096)                                \
+      g_coop_trace[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();  \
+  } while (0)
+extern "C" __attribute__((visibility("default"))) int dpf_amd_debug_coop_trace(void* host,
+                                                                               int64_t bytes) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_coop_trace), (size_t)bytes, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#else
+#define DPF_COOP_MARK(i) \
+  do {                   \
+  } while (0)
+#endif
+#ifndef DPF_COOP_TRACE_SYNC
+#define DPF_COOP_TRACE_SYNC 1
+#endif
 static_assert(kCoopBlock == 1024, "the BFS levels assume 1024 threads (64 -> 1024 nodes)");
 constexpr int kCoopLog = 10;  // log2 nodes after the BFS
 
@@ -436,8 +466,10 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
   __shared__ uint4 nodes[kCoopBlock / 2];
   constexpr int BN = Em::kBN;
   constexpr int K = kCoopLog + E;  // log2 tree leaves per block
+  DPF_COOP_MARK(0);
   FillTables(tab);
   __syncthreads();
+  DPF_COOP_MARK(1);
   const Lds L = MakeLds(tab);
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -476,10 +508,41 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
     reinterpret_cast<uint32_t*>(nodes)[q * 4 + c] = c == 0 ? (x | t) : x;
   }
   __syncthreads();
-  // 2. breadth-first: level j has 128 << j children, child c of parent c / 2
+  DPF_COOP_MARK(2);
+  // 2. breadth-first: level j has 128 << j children, child c of parent c / 2.
+  // The first DPF_COOP_QUAD_BFS levels (128 and 256 children: half and all
+  // of the block as quads) run as quad steps like the walk — a lone lane-AES
+  // at 2-4 waves per CU is latency-bound (~2.9 us per level measured,
+  // tools/coop_trace.py); the rest one child per thread.
+#if DPF_COOP_QUAD_BFS > 0
+  {
+    const int c = lane & 3;
+    const int qd = tid >> 2;
+    const QuadKey kl = MakeQuadKey<0>(c);
+    const QuadDiff kd = MakeQuadDiff(c);
+    const uint32_t* cw_words = reinterpret_cast<const uint32_t*>(a.cw_seed);
+    uint32_t* nw = reinterpret_cast<uint32_t*>(nodes);
+#pragma unroll
+    for (int j = 0; j < DPF_COOP_QUAD_BFS; ++j) {
+      const bool active = wave < (8 << j);  // 128 << j quads, 16 per wave
+      uint32_t xq = 0u, tq = 0u;
+      if (active) {
+        const uint32_t w = nw[(qd >> 1) * 4 + c];
+        tq = QuadPerm<kQuadBcast<0>>(w) & 1u;
+        xq = c == 0 ? (w & ~1u) : w;
+        const int64_t ci = cw0 + s + 6 + j;
+        QuadWalkStep(xq, tq, (uint32_t)qd & 1u, cw_words[ci * 4 + c], a.ccl[ci], a.ccr[ci], c,
+                     kl, kd, L);
+      }
+      __syncthreads();  // every parent of this level has been read
+      if (active) nw[qd * 4 + c] = c == 0 ? (xq | tq) : xq;
+      __syncthreads();
+    }
+  }
+#endif
   uint32_t x[4] = {0u, 0u, 0u, 0u}, t = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = DPF_COOP_QUAD_BFS; j < 4; ++j) {
     const bool active = wave < (2 << j);  // wave-uniform
     if (active) {
       const uint4 p = nodes[tid >> 1];
@@ -498,6 +561,7 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
       __syncthreads();
     }
   }
+  DPF_COOP_MARK(3);
   // 3. leaves: hash, convert, correct, store
   ExpandArgs ak = a;
   if constexpr (kBatched) ak.out += key * a.key_out_stride;
@@ -537,6 +601,7 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
       Em::Emit(Ec, h[0], tr, g0 + 2 * tid + 1);
     }
   }
+  DPF_COOP_MARK(4);
 }
 
 template <int E, class Em>

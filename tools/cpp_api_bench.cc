@@ -215,7 +215,7 @@ void C4(int reps) {
   auto dpf = DistributedPointFunction::Create(p);
   OK_OR_DIE(dpf);
   std::mt19937_64 rng(4);
-  for (int q : {1, 8, 64}) {
+  for (int q : {1, 8, 64, 100}) {
     PirRequest req[2];
     std::vector<int64_t> idx(q);
     for (int k = 0; k < q; ++k) {
