@@ -427,7 +427,7 @@ int LaunchExpand(int, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
 #endif
 constexpr int kCoopBlock = DPF_COOP_BLOCK;
 #ifndef DPF_COOP_QUAD_BFS
-#define DPF_COOP_QUAD_BFS 0  // breadth-first levels run as quad steps (0-2)
+#define DPF_COOP_QUAD_BFS 2  // breadth-first levels run as quad steps (0-2; 2: c1 span 38.9 -> 36.5 us)
 #endif
 static_assert(DPF_COOP_QUAD_BFS >= 0 && DPF_COOP_QUAD_BFS <= 2, "quad BFS levels: 0-2");
 
@@ -513,7 +513,8 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
   // The first DPF_COOP_QUAD_BFS levels (128 and 256 children: half and all
   // of the block as quads) run as quad steps like the walk — a lone lane-AES
   // at 2-4 waves per CU is latency-bound (~2.9 us per level measured,
-  // tools/coop_trace.py); the rest one child per thread.
+  // tools/coop_trace.py; the four levels 11.7 -> 9.7 us with two quad levels,
+  // profiles/coop_quad_bfs_r03r.log); the rest one child per thread.
 #if DPF_COOP_QUAD_BFS > 0
   {
     const int c = lane & 3;
