@@ -192,3 +192,37 @@ def test_batch_matches_single_and_errors(cuda):
     with pytest.raises(DpfAmdError) as e:
         dcf.evaluate(DcfKey(b""), 0)
     assert e.value.code == 3 and "key" in str(e.value)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec,n", [(("int", 64), 32), (("int", 8), 20), (("int", 128), 16),
+                                    (("xor", 64), 24)], ids=lambda x: repr(x))
+def test_batch_evaluate_many_pairs_kernels_agree(cuda, spec, n):
+    """Thousands of (key, point) pairs over many waves, both parties: the
+    automatic kernel (the register-only one for these single scalars) equals
+    the generic kernel bit for bit, and the shares of integer types
+    reconstruct beta on x < alpha, 0 elsewhere."""
+    from distributed_point_functions_amd import kernels as K
+    rng = random.Random(n * 7 + len(spec))
+    dcf = _dcf(spec, n)
+    vt = V.from_spec(spec)
+    beta = _beta42(spec)
+    keys0, keys1, xs, alphas = [], [], [], []
+    for j in range(24):
+        alpha = rng.randrange(1 << n)
+        k0, k1 = dcf.generate_keys(alpha, beta, seeds=(2 * j + 11, 2 * j + 12))
+        pts = [rng.randrange(1 << n) for _ in range(200)]
+        pts += [max(alpha - 1, 0), alpha, min(alpha + 1, (1 << n) - 1)]
+        keys0 += [k0] * len(pts)
+        keys1 += [k1] * len(pts)
+        xs += pts
+        alphas += [alpha] * len(pts)
+    with K.forced_dcf_kernel(0):
+        a0, a1 = dcf.batch_evaluate(keys0, xs), dcf.batch_evaluate(keys1, xs)
+    with K.forced_dcf_kernel(1):
+        g0, g1 = dcf.batch_evaluate(keys0, xs), dcf.batch_evaluate(keys1, xs)
+    assert a0 == g0 and a1 == g1
+    if spec[0] == "int":
+        zero = vt.zero()
+        for x, al, r0, r1 in zip(xs, alphas, a0, a1):
+            assert vt.add(r0, r1) == (beta if x < al else zero), (x, al)
