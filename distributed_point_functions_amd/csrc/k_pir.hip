@@ -460,6 +460,9 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
 #ifndef DPF_SCAN_M4_DUAL
 #define DPF_SCAN_M4_DUAL 1
 #endif
+#ifndef DPF_SCAN_M4_DUAL_PF
+#define DPF_SCAN_M4_DUAL_PF 1  // steps of 8 records in flight per wave at P = 2
+#endif
 #ifndef DPF_SCAN_M4_DUAL_RB
 #define DPF_SCAN_M4_DUAL_RB 4  // row-pair reads in flight (8 VGPRs each)
 #endif
@@ -517,11 +520,12 @@ __device__ __forceinline__ void ScanM4Tile2(const ScanArgs& a, int64_t tile, uin
   auto load = [&](int r) -> uint32_t {
     return __builtin_amdgcn_raw_buffer_load_b32(rsrc, col_ok ? voff + r * rec_bytes : voff, 0, 2);
   };
-  // the next 8 records in flight; the last step re-reads the tile's first
-  // (cached) records rather than branching
-  uint32_t xq[8];
+  // the next DPF steps' records (8 each) in flight; the last steps re-read
+  // the tile's first (cached) records rather than branching
+  constexpr int DPF = P == 2 ? DPF_SCAN_M4_DUAL_PF : 1;
+  uint32_t xq[8 * DPF];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) xq[i] = load(i);
+  for (int i = 0; i < 8 * DPF; ++i) xq[i] = load(i);
 #pragma unroll 1
   for (int k = 0; k < 16; ++k) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -534,7 +538,9 @@ __device__ __forceinline__ void ScanM4Tile2(const ScanArgs& a, int64_t tile, uin
       xb[i] = xq[4 + i];
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) xq[i] = load((8 * (k + 1) + i) & 127);
+    for (int i = 0; i < 8 * (DPF - 1); ++i) xq[i] = xq[i + 8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xq[8 * (DPF - 1) + i] = load((8 * (k + DPF) + i) & 127);
     DPF_M4_STORE_TABLE(0, xa);
     DPF_M4_STORE_TABLE(4352, xb);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
