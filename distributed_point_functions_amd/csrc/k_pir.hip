@@ -339,6 +339,9 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
 #ifndef DPF_SCAN_M4_ADDTID
 #define DPF_SCAN_M4_ADDTID 1  // row stores as ds_write_addtid_b32 (inline asm)
 #endif
+#ifndef DPF_SCAN_M4_WORD_LOOPS
+#define DPF_SCAN_M4_WORD_LOOPS 1  // P = 2 / 4: per-word loops unrolled by two
+#endif
 #ifndef DPF_SCAN_M4_PREFETCH
 #define DPF_SCAN_M4_PREFETCH 1  // 4-record groups in flight per wave
 #endif
@@ -379,8 +382,8 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
   uint32_t xq[4 * PF];
 #pragma unroll
   for (int i = 0; i < 4 * PF; ++i) xq[i] = load(i);
-#pragma unroll 1
-  for (int k = 0; k < 32; ++k) {
+  // step k: records 4k..4k+3, table row e
+  auto step = [&](int k, int e) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -431,8 +434,6 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint32_t word = SelWord(s, k >> 3);
-    const int e = (word >> (4 * (k & 7))) & 15;
     const uint4* row = reinterpret_cast<const uint4*>(t) + e * ROW + cpart * CPL;
     // row reads in batches of RB (their destination VGPRs are what bounds
     // the wave's register budget)
@@ -448,6 +449,22 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
         acc[4 * c + 3] ^= v.w;
       }
       if (RB < CPL) __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  if constexpr (!DPF_SCAN_M4_WORD_LOOPS) {
+#pragma unroll 1
+    for (int k = 0; k < 32; ++k) step(k, (SelWord(s, k >> 3) >> (4 * (k & 7))) & 15);
+  } else {
+    // One loop per selection word, two steps per iteration: a word picked by
+    // the step index made the compiler lower the pick to a branch tree,
+    // split the loop and copy the prefetched registers at the back edge
+    // behind an s_waitcnt vmcnt(0) — every step then waited for its own
+    // prefetch, one HBM latency per 4 records.
+#pragma unroll
+    for (int wi = 0; wi < 4; ++wi) {
+      const uint32_t word = wi == 0 ? s.x : wi == 1 ? s.y : wi == 2 ? s.z : s.w;
+#pragma unroll 2
+      for (int kk = 0; kk < 8; ++kk) step(wi * 8 + kk, (word >> (4 * kk)) & 15);
     }
   }
 }
@@ -526,8 +543,8 @@ __device__ __forceinline__ void ScanM4Tile2(const ScanArgs& a, int64_t tile, uin
   uint32_t xq[8 * DPF];
 #pragma unroll
   for (int i = 0; i < 8 * DPF; ++i) xq[i] = load(i);
-#pragma unroll 1
-  for (int k = 0; k < 16; ++k) {
+  // step k: records 8k..8k+7 into tables A and B, selection byte sb
+  auto step = [&](int k, uint32_t sb) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -546,8 +563,7 @@ __device__ __forceinline__ void ScanM4Tile2(const ScanArgs& a, int64_t tile, uin
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // groups 2k and 2k + 1: one selection byte, low nibble for table A
-    const uint32_t sb = (SelWord(s, k >> 2) >> (8 * (k & 3))) & 255;
+    // groups 2k and 2k + 1: low nibble for table A
     const uint4* ra = reinterpret_cast<const uint4*>(t) + (sb & 15) * ROW + cpart * CPL;
     const uint4* rb = reinterpret_cast<const uint4*>(t) + (16 + (sb >> 4)) * ROW + cpart * CPL;
     constexpr int RB = CPL < DPF_SCAN_M4_DUAL_RB ? CPL : DPF_SCAN_M4_DUAL_RB;
@@ -563,14 +579,30 @@ __device__ __forceinline__ void ScanM4Tile2(const ScanArgs& a, int64_t tile, uin
       }
       if (RB < CPL) __builtin_amdgcn_sched_barrier(0);
     }
+  };
+  if constexpr ((P == 1 && DPF_SCAN_M4_WORD_LOOPS < 2) || !DPF_SCAN_M4_WORD_LOOPS) {
+    // (P = 1 at 126 VGPRs: the two-step word loops below spill)
+#pragma unroll 1
+    for (int k = 0; k < 16; ++k) step(k, (SelWord(s, k >> 2) >> (8 * (k & 3))) & 255);
+  } else {
+    // one loop per selection word, two steps per iteration (see ScanM4Tile)
+#pragma unroll
+    for (int wi = 0; wi < 4; ++wi) {
+      const uint32_t word = wi == 0 ? s.x : wi == 1 ? s.y : wi == 2 ? s.z : s.w;
+#pragma unroll 2
+      for (int kk = 0; kk < 4; ++kk) step(wi * 4 + kk, (word >> (8 * kk)) & 255);
+    }
   }
 }
 
+#ifndef DPF_SCAN_M4_P4_WAVES
+#define DPF_SCAN_M4_P4_WAVES 8  // 8192 parts = one resident round at 8 waves/SIMD
+#endif
 #ifndef DPF_SCAN_M4_P1_WAVES
 #define DPF_SCAN_M4_P1_WAVES 4  // 100 VGPRs (5 waves: 4 spilled, Q = 64 4.31 vs 4.36 ms)
 #endif
 template <int P>
-__global__ __launch_bounds__(kScanM4Block, P == 1 ? DPF_SCAN_M4_P1_WAVES : P == 2 ? 4 : 6)
+__global__ __launch_bounds__(kScanM4Block, P == 1 ? DPF_SCAN_M4_P1_WAVES : P == 2 ? 4 : DPF_SCAN_M4_P4_WAVES)
 void KPirScanM4(ScanArgs a) {
   constexpr int QW = 64 / P;        // queries per wave
   constexpr int CPL = 16 / P;       // 16-byte columns of the slice per lane
