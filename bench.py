@@ -280,18 +280,19 @@ def bench_handle_request(args, n, rec, db_tensor, device, shard_devices=None,
 def bench_in_process(args):
     """All N GPUs from one process through the library's multi-GPU API."""
     from distributed_point_functions_amd import pir as P
-    ngpu = args.gpus
-    devs = list(range(ngpu))
+    devs = ([int(d) for d in args.devices.split(",")] if args.devices
+            else list(range(args.gpus)))
+    ngpu = len(devs)
     vt = V.Tuple(V.Integer(32), V.IntModN(64, P64))
     dpf = DistributedPointFunction.create(DpfParameters(args.log_domain, vt, 48))
     alpha = 0x9E3779B9 % (1 << args.log_domain)
     k0, _ = dpf.generate_keys(alpha, (123456789, 987654321), seeds=(0xA5A5, 0x5A5A))
     total = 1 << dpf.hierarchy_to_tree(0)
     slices = []
-    for r in devs:
-        lo, hi = sharding.block_range(total, ngpu, r)
-        slices.append((r, lo, hi, torch.empty((hi - lo) * 16, dtype=torch.uint8,
-                                              device=torch.device("cuda", r))))
+    for i, d in enumerate(devs):
+        lo, hi = sharding.block_range(total, ngpu, i)
+        slices.append((d, lo, hi, torch.empty((hi - lo) * 16, dtype=torch.uint8,
+                                              device=torch.device("cuda", d))))
     for _ in range(args.warmup):
         dpf.expand_leaves_on_devices(k0, slices)
     t0 = time.perf_counter()
@@ -317,25 +318,43 @@ def library_sha256():
         return hashlib.sha256(f.read()).hexdigest()
 
 
-def traffic_from_profiles(kernel_substr):
-    """(HBM bytes per launch, profile file) of a kernel from a committed PMC
+def traffic_from_profiles(kernel_re):
+    """(HBM bytes per launch, profile file, PMC entry, error) of the kernel
+    whose demangled name matches the regex `kernel_re`, from a committed PMC
     summary of THIS build (profiles/<round>_pmc.json, written by
     tools/summarize_profile.py from separate rocprofv3 --pmc FETCH_SIZE /
     WRITE_SIZE passes of this bench, keyed by the profiled library's
-    sha256); (None, None) when no summary matches the loaded library."""
+    sha256).  When nothing matches, the first three are None and `error`
+    says why (no summary of this library, or the kernel is not in it), so
+    the bench line never carries a silent null."""
     import glob
+    import re
+    pat = re.compile(kernel_re)
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                           "profiles", "r*_pmc.json")), key=os.path.getmtime)
     sha = library_sha256()
+    keyed = []
     for f in reversed(files):
         with open(f) as fh:
             d = json.load(fh)
         if d.get("_meta", {}).get("library_sha256") != sha:
             continue
+        keyed.append(os.path.basename(f))
         for name, e in d.items():
-            if kernel_substr in name and "hbm_bytes" in e:
-                return e["hbm_bytes"], os.path.basename(f), e
-    return None, None, None
+            if pat.search(name) and isinstance(e, dict) and "hbm_bytes" in e:
+                return e["hbm_bytes"], os.path.basename(f), e, None
+    if not keyed:
+        err = ("no profiles/r*_pmc.json is keyed to the loaded library (sha256 %s): "
+               "profile this build with tools/profile_gpu.sh" % sha[:16])
+    else:
+        err = "kernel /%s/ not found in %s" % (kernel_re, ", ".join(keyed))
+    return None, None, None, err
+
+
+# Demangled kernel names as rocprofv3 reports them; template arguments after
+# the ones that identify the launch are matched loosely.
+EXPAND_C5_KERNEL_RE = r"KExpand<8, dpf_amd::EmitU32ModN64(, [^>]*)?>"
+SCAN_Q1_KERNEL_RE = r"KPirScanG<1, 4(, [^>]*)?>"
 
 
 def clock_view(entry):
@@ -417,11 +436,19 @@ def main():
     ap.add_argument("--skip-cpu-baseline", action="store_true")
     ap.add_argument("--skip-pir", action="store_true")
     ap.add_argument("--skip-handle-request", action="store_true")
+    ap.add_argument("--devices", default="",
+                    help="--in-process: comma-separated device list, one slice / shard per entry "
+                         "(entries may repeat: a rehearsal of N devices' code on fewer GPUs)")
+    ap.add_argument("--force-peer", action="store_true",
+                    help="--in-process: take the cross-device copy branches even between "
+                         "slices on one device (dpf_amd_set_force_peer_copies)")
     ap.add_argument("--in-process", action="store_true",
                     help="drive all --gpus GPUs from this one process through the library's "
                          "multi-GPU API (ExpandLeavesOnDevices, a sharded DenseDpfPirDatabase)")
     args = ap.parse_args()
     if args.in_process:
+        if args.force_peer:
+            _lib.lib().dpf_amd_set_force_peer_copies(1)
         return main_in_process(args)
     world, rank, device = setup()
     r = bench_dpf(args, world, rank, device)
@@ -437,9 +464,9 @@ def main():
         aes_s = aes_per_launch / (r["kernel_ms"] / 1e3)
         achieved = aes_s * OPS_PER_AES / 1e12
         lookups_s = LDS_LOOKUPS_PER_LEAF_C5 * (leaves / world) / (r["kernel_ms"] / 1e3)
-        expand_traffic = traffic_from_profiles("KExpand<8, dpf_amd::EmitU32ModN64>")
+        expand_traffic = traffic_from_profiles(EXPAND_C5_KERNEL_RE)
         clk = clock_view(expand_traffic[2])
-        scan_traffic = traffic_from_profiles("KPirScanG<1, 4>")
+        scan_traffic = traffic_from_profiles(SCAN_Q1_KERNEL_RE)
         out = {
             "metric": METRIC, "value": value, "unit": "leaves/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
@@ -461,6 +488,7 @@ def main():
                          "frac": lookups_s / LDS_PEAK_LOOKUPS,
                          "traffic": expand_traffic[0],
                          "traffic_unit": "HBM bytes per launch (rocprofv3 PMC of this build)",
+                         "traffic_error": expand_traffic[3],
                          "traffic_profile": expand_traffic[1],
                          "algorithmic_bytes": leaves // world * 16,
                          "kernel": "KExpand<8,EmitU32ModN64>", "kernel_ms": r["kernel_ms"],
@@ -496,6 +524,7 @@ def main():
                 "roofline": {"bound": "hbm", "achieved": scan_gbs, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": scan_gbs / HBM_PEAK_GBS,
                              "traffic": scan_traffic[0], "traffic_profile": scan_traffic[1],
+                             "traffic_error": scan_traffic[3],
                              "algorithmic_bytes": pir["per_gpu_bytes"],
                              "kernel": "KPirScanG<1,4>+KXorFold", "kernel_ms": pir["scan_ms"]},
                 "batch_%d" % pir["mq"]: {
@@ -519,7 +548,12 @@ def main():
 
 def main_in_process(args):
     r = bench_in_process(args)
+    devs = [int(d) for d in args.devices.split(",")] if args.devices else list(range(args.gpus))
+    args.gpus = len(set(devs))  # distinct GPUs; slices on a repeated device share it
     ms = 1000 * r["wall"] / args.steps
+    per_gpu_leaves = r["leaves"] / args.gpus
+    lookups_s = LDS_LOOKUPS_PER_LEAF_C5 * per_gpu_leaves / (ms / 1e3)
+    expand_traffic = traffic_from_profiles(EXPAND_C5_KERNEL_RE)
     out = {
         "metric": METRIC, "value": r["leaves"] / (r["wall"] / args.steps), "unit": "leaves/s",
         "n_gpus": args.gpus, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
@@ -530,15 +564,42 @@ def main_in_process(args):
                                % args.log_domain,
                    "leaves_per_step": r["leaves"], "tree_levels": r["L"],
                    "parallelism": "in-process: DistributedPointFunction::ExpandLeavesOnDevices "
-                                  "over %d GPU(s), disjoint subtree slices" % args.gpus},
+                                  "over %d GPU(s), disjoint subtree slices" % args.gpus,
+                   "devices": devs},
+        # per GPU: its slice's lookups over the step's wall time (the launch
+        # and the wait for every device included, so a lower bound)
+        "roofline": {"bound": "lds", "achieved": lookups_s / 1e12,
+                     "peak": LDS_PEAK_LOOKUPS / 1e12, "unit": "T lookups/s",
+                     "frac": lookups_s / LDS_PEAK_LOOKUPS,
+                     "traffic": expand_traffic[0], "traffic_profile": expand_traffic[1],
+                     "traffic_error": expand_traffic[3],
+                     "algorithmic_bytes": int(per_gpu_leaves) * 16,
+                     "kernel": "KExpand<8,EmitU32ModN64>", "kernel_ms": ms,
+                     "kernel_ms_is": "step wall time of ExpandLeavesOnDevices",
+                     "lookups_per_leaf": LDS_LOOKUPS_PER_LEAF_C5},
+        "cpu_baseline": None,
     }
     if r["pir"]:
         p = r["pir"]
-        out["pir"] = {"api": "DenseDpfPirServer::HandleRequest, database sharded over %d GPU(s)"
-                             % args.gpus,
+        q1 = p["ms"][1]
+        per_gpu_bytes = p["n"] * p["rec"] / args.gpus
+        gbs = per_gpu_bytes / (q1 / 1e3) / 1e9
+        out["pir"] = {"api": "DenseDpfPirServer::HandleRequest, database sharded over devices %s"
+                             % devs,
+                      "metric": "dense-PIR scan GB/s", "unit": "GB/s",
+                      "value": p["n"] * p["rec"] / (q1 / 1e3) / 1e9,
                       "ms_per_request": {str(q): v for q, v in p["ms"].items()},
-                      "db_GBps_at_q1": p["n"] * p["rec"] / (p["ms"][1] / 1e3) / 1e9,
-                      "correct": p["ok"]}
+                      "db_GBps_at_q1": p["n"] * p["rec"] / (q1 / 1e3) / 1e9,
+                      "correct": p["ok"], "scaling": "strong",
+                      # per GPU: its shard's bytes over the whole Q = 1
+                      # request (decode, expansion, scan, peer-copied
+                      # partials, fold, encode) — a lower bound on the scan's
+                      "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
+                                   "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                                   "algorithmic_bytes": per_gpu_bytes,
+                                   "kernel": "KPirScanG<1,4>+KXorFold",
+                                   "kernel_ms": q1,
+                                   "kernel_ms_is": "HandleRequest wall time at Q = 1"}}
     print(json.dumps(out), flush=True)
 
 

@@ -89,6 +89,8 @@ def lib():
     _sig(L, "dpf_amd_version", ctypes.c_char_p)
     _sig(L, "dpf_amd_device_count", I32, ctypes.POINTER(ctypes.c_int))
     _sig(L, "dpf_amd_release_cached_memory", I32, ctypes.POINTER(I64))
+    _sig(L, "dpf_amd_set_thread_cache_cap", I32, I32)
+    _sig(L, "dpf_amd_set_force_peer_copies", None, I32)
     _sig(L, "dpf_amd_free", None, P)
     _sig(L, "dpf_amd_aes128_mmo", I32, U64, U64, P, P, I64, P)
     _sig(L, "dpf_amd_evaluate_seeds", I32, I64, I32, I64, P, P, P, I32, P, P, P,
@@ -145,6 +147,7 @@ def _bind_tier2(L):
     _sig(L, "dpf_amd_evaluate_until_device", I32, P, I32, P, I64, P, SZ, P, P, I64,
          ctypes.POINTER(I64), P)
     _sig(L, "dpf_amd_evaluate_at", I32, P, P, SZ, I32, P, I64, P, SZ, P)
+    _sig(L, "dpf_amd_evaluate_at_ctx", I32, P, I32, P, I64, P, SZ, P, P)
     _sig(L, "dpf_amd_expand_leaves_on_devices", I32, P, P, SZ, I32, P, P, P, P)
     _sig(L, "dpf_amd_evaluate_and_apply", I32, P, P, P, I64, P, I32, P, SZ, P, APPLY_FN, P)
     _sig(L, "dpf_amd_dcf_create", I32, P, SZ, PP)

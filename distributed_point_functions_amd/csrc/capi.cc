@@ -273,6 +273,25 @@ int dpf_amd_evaluate_at(const dpf_amd_dpf* dpf, const uint8_t* key, size_t key_l
   return st.ok() ? DPF_AMD_OK : Fail(st);
 }
 
+int dpf_amd_evaluate_at_ctx(const dpf_amd_dpf* dpf, int hierarchy_level, const uint64_t* points,
+                            int64_t num_points, const uint8_t* value_type, size_t value_type_len,
+                            dpf_amd_ctx* ctx, void* out) {
+  if (!dpf || !ctx) return Fail(DPF_AMD_INVALID_ARGUMENT, "null handle");
+  ValueType t;
+  int rc = ParseType(value_type, value_type_len, &t);
+  if (rc != DPF_AMD_OK) return rc;
+  Status st = dpf->dpf->CheckType(t, hierarchy_level, true);
+  if (!st.ok()) return Fail(st);
+  std::vector<uint128> p = ToU128(points, num_points);
+  const int lvl = (hierarchy_level >= 0 && hierarchy_level < dpf->dpf->num_hierarchy_levels())
+                      ? hierarchy_level
+                      : 0;
+  st = dpf->dpf->EvaluateAtRaw(ctx->ctx.key(), hierarchy_level,
+                               Span<const uint128>(p.data(), p.size()), &ctx->ctx,
+                               dpf->dpf->value_type_descriptor(lvl), out);
+  return st.ok() ? DPF_AMD_OK : Fail(st);
+}
+
 int dpf_amd_evaluate_and_apply(const dpf_amd_dpf* dpf, const uint8_t* const* keys,
                                const size_t* key_lengths, int64_t num_keys,
                                const uint64_t* points, int rightshift,

@@ -1886,6 +1886,7 @@ Status DistributedPointFunction::ExpandLeavesOnDevices(const DpfKey& key, Span<c
     return InvalidArgumentError("`devices`, `leaf_begin`, `leaf_end` and `outs` must have the "
                                 "same size");
   DPF_RETURN_IF_ERROR(ValidateDpfKey(*state_, key));
+  for (int d : devices) DPF_RETURN_IF_ERROR(dpf_internal_host::CheckDevice(d));
   // Issue every device's launch first (each on this thread's stream for that
   // device), then wait for all of them.
   Status st = OkStatus();

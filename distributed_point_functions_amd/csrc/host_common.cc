@@ -5,6 +5,7 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <string>
 
 #include "dpf_amd.h"
@@ -27,13 +28,37 @@ namespace {
 // DPF_AMD_SEGV_BACKTRACE=1 (diagnostics): on SIGSEGV / SIGBUS / SIGABRT
 // print the faulting thread's native stack to stderr (a host process's
 // Python faulthandler shows only Python frames), then hand the signal to
-// the previous handler.
+// the previous handler.  The handler only calls async-signal-safe code:
+// write(2) of a message built by hand, and backtrace(), whose first call
+// (which loads libgcc_s and allocates) already happened when the handler
+// was installed.
 struct sigaction g_prev[32];
+size_t AppendStr(char* buf, size_t at, size_t cap, const char* s) {
+  while (*s && at + 1 < cap) buf[at++] = *s++;
+  return at;
+}
+size_t AppendHex(char* buf, size_t at, size_t cap, uintptr_t v) {
+  char tmp[2 + 2 * sizeof(uintptr_t)];
+  int k = 0;
+  do {
+    tmp[k++] = "0123456789abcdef"[v & 15];
+    v >>= 4;
+  } while (v && k < static_cast<int>(sizeof tmp));
+  at = AppendStr(buf, at, cap, "0x");
+  while (k > 0 && at + 1 < cap) buf[at++] = tmp[--k];
+  return at;
+}
 void OnFatal(int sig, siginfo_t* info, void* uctx) {
   char msg[128];
-  const int n = snprintf(msg, sizeof msg, "[dpf_amd] signal %d at address %p, thread stack:\n",
-                         sig, info ? info->si_addr : nullptr);
-  if (n > 0) (void)!write(2, msg, static_cast<size_t>(n));
+  size_t n = AppendStr(msg, 0, sizeof msg, "[dpf_amd] signal ");
+  if (n + 3 < sizeof msg) {
+    if (sig >= 10) msg[n++] = static_cast<char>('0' + (sig / 10) % 10);
+    msg[n++] = static_cast<char>('0' + sig % 10);
+  }
+  n = AppendStr(msg, n, sizeof msg, " at address ");
+  n = AppendHex(msg, n, sizeof msg, reinterpret_cast<uintptr_t>(info ? info->si_addr : nullptr));
+  n = AppendStr(msg, n, sizeof msg, ", thread stack:\n");
+  (void)!write(2, msg, n);
   void* frames[64];
   const int k = backtrace(frames, 64);
   backtrace_symbols_fd(frames, k, 2);
@@ -49,6 +74,8 @@ void OnFatal(int sig, siginfo_t* info, void* uctx) {
 }
 const bool g_segv_trace = [] {
   if (!getenv("DPF_AMD_SEGV_BACKTRACE")) return false;
+  void* warm[4];
+  (void)backtrace(warm, 4);  // loads libgcc_s now, not inside the handler
   struct sigaction sa;
   memset(&sa, 0, sizeof sa);
   sa.sa_sigaction = OnFatal;
@@ -57,7 +84,18 @@ const bool g_segv_trace = [] {
   for (int sig : {SIGSEGV, SIGBUS, SIGABRT}) sigaction(sig, &sa, &g_prev[sig]);
   return true;
 }();
+
+// Idle per-thread resource objects kept for future threads (ThreadRecycled,
+// host_device.h); DPF_AMD_THREAD_CACHE or dpf_amd_set_thread_cache_cap.
+std::atomic<int> g_thread_cache_cap{[] {
+  const char* e = getenv("DPF_AMD_THREAD_CACHE");
+  return e ? atoi(e) : 64;
+}()};
+std::atomic<int> g_force_peer_copies{0};
 }  // namespace
+
+int ThreadCacheCap() { return g_thread_cache_cap.load(std::memory_order_relaxed); }
+bool ForcePeerCopies() { return g_force_peer_copies.load(std::memory_order_relaxed) != 0; }
 
 }  // namespace dpf_amd
 
@@ -66,5 +104,13 @@ extern "C" {
 const char* dpf_amd_last_error(void) { return dpf_amd::LastError(); }
 
 void dpf_amd_free(void* p) { free(p); }
+
+int dpf_amd_set_thread_cache_cap(int cap) {
+  if (cap < 0) return dpf_amd::SetError(DPF_AMD_INVALID_ARGUMENT, "cap must be >= 0");
+  dpf_amd::g_thread_cache_cap.store(cap);
+  return DPF_AMD_OK;
+}
+
+void dpf_amd_set_force_peer_copies(int on) { dpf_amd::g_force_peer_copies.store(on ? 1 : 0); }
 
 }  // extern "C"

@@ -43,12 +43,15 @@ inline Status AbiStatus(int rc) {
 // recycled through a process-wide free list when their thread exits instead
 // of being destroyed: a server answering from many short-lived threads pays
 // for stream / pinned-memory creation once per concurrent thread, not once
-// per thread, and no HIP call runs in a thread-exit handler (destroying them
-// there — pinned frees and event syncs from dozens of exiting threads while
-// others launch work — is what the runtime crashed on in round 3's 128-thread
-// test).  Every recycled object waits for its own in-flight work before it
-// reuses a buffer, so a new owner thread inherits it safely.  The objects
-// are never destroyed (no HIP calls at process exit).
+// per thread, and no HIP call runs in a thread-exit handler.  (Round 3's
+// 128-thread test crashed in the runtime while per-thread objects were
+// destroyed in exit handlers and other threads launched work; that run's
+// output was not kept, so the exit handlers are the suspected, not the
+// proven, cause — DESIGN.md §5.)  Every recycled object waits for its own
+// in-flight work before it reuses a buffer, so a new owner thread inherits it
+// safely.  At most ThreadCacheCap() idle objects of a kind are kept; an exit
+// handler parks the surplus, and the next thread to take an object (in its
+// first Get, a live thread) destroys it.
 template <class T>
 class ThreadRecycled {
  public:
@@ -56,11 +59,17 @@ class ThreadRecycled {
     thread_local Holder h;
     return *h.p;
   }
+  // Idle objects kept for future threads, and surplus awaiting destruction.
+  static std::pair<size_t, size_t> Idle() {
+    std::lock_guard<std::mutex> l(P().mu);
+    return {P().free.size(), P().surplus.size()};
+  }
 
  private:
   struct Pool {
     std::mutex mu;
     std::vector<T*> free;
+    std::vector<T*> surplus;
   };
   static Pool& P() {
     static Pool* p = new Pool();
@@ -69,18 +78,22 @@ class ThreadRecycled {
   struct Holder {
     T* p = nullptr;
     Holder() {
+      std::vector<T*> drop;
       {
         std::lock_guard<std::mutex> l(P().mu);
         if (!P().free.empty()) {
           p = P().free.back();
           P().free.pop_back();
         }
+        drop.swap(P().surplus);
       }
+      for (T* x : drop) delete x;  // outside the lock, in a live thread
       if (p == nullptr) p = new T();
     }
     ~Holder() {
       std::lock_guard<std::mutex> l(P().mu);
-      P().free.push_back(p);
+      const size_t cap = static_cast<size_t>(std::max(0, dpf_amd::ThreadCacheCap()));
+      (P().free.size() < cap ? P().free : P().surplus).push_back(p);
     }
   };
 };
@@ -90,19 +103,45 @@ class ThreadRecycled {
 class DeviceGuard {
  public:
   explicit DeviceGuard(int device) {
-    if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
-    if (device >= 0 && device != prev_ && hipSetDevice(device) == hipSuccess) set_ = true;
+    if (hipGetDevice(&prev_) != hipSuccess) {
+      prev_ = -1;
+      (void)hipGetLastError();
+    }
+    if (device >= 0 && device != prev_) {
+      if (hipSetDevice(device) == hipSuccess) {
+        set_ = true;
+      } else {
+        ok_ = false;
+        (void)hipGetLastError();  // not left sticky for the next launch check
+      }
+    }
   }
   ~DeviceGuard() {
     if (set_ && prev_ >= 0) (void)hipSetDevice(prev_);
   }
   DeviceGuard(const DeviceGuard&) = delete;
   DeviceGuard& operator=(const DeviceGuard&) = delete;
+  // false when the device could not be made current
+  bool ok() const { return ok_; }
 
  private:
   int prev_ = -1;
   bool set_ = false;
+  bool ok_ = true;
 };
+
+// INVALID_ARGUMENT unless 0 <= device < the number of visible devices.
+inline Status CheckDevice(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    n = 0;
+  }
+  if (device < 0 || device >= n)
+    return InvalidArgumentError("invalid device id " + std::to_string(device) + " (" +
+                                std::to_string(n) + " visible)");
+  return OkStatus();
+}
 
 // The calling thread's stream number `index` on `device` (sharded
 // databases and multi-GPU expansions issue each device's work on its own
@@ -117,8 +156,12 @@ inline hipStream_t ThreadStreamOn(int device, int index = 0) {
   auto it = h.s.find(key);
   if (it != h.s.end()) return it->second;
   DeviceGuard g(device);
+  if (!g.ok()) return nullptr;  // never file a stream of another device under `device`
   hipStream_t st = nullptr;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
   h.s[key] = st;
   return st;
 }
@@ -196,7 +239,14 @@ class HostPool {
       if (parts == 1) fn(size_t{0});
       return;
     }
-    std::lock_guard<std::mutex> one(call_mu_);
+    // Another thread's job holds the workers: run this one inline rather
+    // than queue behind it (a many-thread server's host loops and pinned
+    // copies then proceed side by side instead of one Run at a time).
+    std::unique_lock<std::mutex> one(call_mu_, std::try_to_lock);
+    if (!one.owns_lock()) {
+      for (size_t i = 0; i < parts; ++i) fn(i);
+      return;
+    }
     Job job{&fn, [](const void* f, size_t i) { (*static_cast<const Fn*>(f))(i); }};
     {
       std::lock_guard<std::mutex> l(mu_);
@@ -610,7 +660,42 @@ class DevicePool {
 
   void Free(void* p, hipStream_t s) {
     if (p == nullptr) return;
+    std::vector<Evicted> evict;
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      FreeLocked(p, s, &evict);
+    }
+    Drop(evict);  // GPU syncs and hipFree without the pool lock
+  }
+
+  // Returns every idle cached block to the device.
+  void Release() {
+    std::vector<Evicted> evict;
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      TakeLocked(0, &evict);
+    }
+    Drop(evict);
+  }
+
+  size_t cached_bytes() {
     std::lock_guard<std::mutex> l(mu_);
+    return cached_;
+  }
+
+ private:
+  struct Block {
+    void* p;
+    size_t size;
+    hipStream_t stream;
+    hipEvent_t ready;
+    uint64_t seq;  // free order (least recently freed is trimmed first)
+  };
+  struct Evicted {
+    int device;
+    Block b;
+  };
+  void FreeLocked(void* p, hipStream_t s, std::vector<Evicted>* evict) {
     auto it = live_.find(p);
     if (it == live_.end()) return;
     Block b{p, it->second.first, s, nullptr, ++seq_};
@@ -632,28 +717,8 @@ class DevicePool {
     }
     free_.emplace(std::make_pair(dev, b.size), b);
     cached_ += b.size;
-    if (cached_ > CacheLimit()) TrimLocked(CacheLimit());
+    if (cached_ > CacheLimit()) TakeLocked(CacheLimit(), evict);
   }
-
-  // Returns every idle cached block to the device.
-  void Release() {
-    std::lock_guard<std::mutex> l(mu_);
-    TrimLocked(0);
-  }
-
-  size_t cached_bytes() {
-    std::lock_guard<std::mutex> l(mu_);
-    return cached_;
-  }
-
- private:
-  struct Block {
-    void* p;
-    size_t size;
-    hipStream_t stream;
-    hipEvent_t ready;
-    uint64_t seq;  // free order (least recently freed is trimmed first)
-  };
   static size_t CacheLimit() {
     static const size_t lim = [] {
       const char* e = std::getenv("DPF_AMD_POOL_CACHE_MB");
@@ -661,9 +726,9 @@ class DevicePool {
     }();
     return lim;
   }
-  // Frees idle blocks, least recently freed first, until at most `keep`
-  // bytes stay cached (caller holds mu_).
-  void TrimLocked(size_t keep) {
+  // Takes idle blocks out of the cache, least recently freed first, until at
+  // most `keep` bytes stay cached (caller holds mu_); Drop frees them.
+  void TakeLocked(size_t keep, std::vector<Evicted>* out) {
     if (cached_ <= keep) return;
     std::vector<std::multimap<std::pair<int, size_t>, Block>::iterator> order;
     order.reserve(free_.size());
@@ -672,14 +737,23 @@ class DevicePool {
               [](const auto& x, const auto& y) { return x->second.seq < y->second.seq; });
     for (auto it : order) {
       if (cached_ <= keep) break;
-      Block& b = it->second;
-      DeviceGuard g(it->first.first);
-      if (b.ready) (void)hipEventSynchronize(b.ready);
-      (void)hipFree(b.p);
-      if (b.ready) events_[it->first.first].push_back(b.ready);
-      cached_ -= b.size;
+      out->push_back(Evicted{it->first.first, it->second});
+      cached_ -= it->second.size;
       free_.erase(it);
     }
+  }
+  // Waits for each evicted block's last use and frees it (no lock held),
+  // then returns the events to the per-device free lists.
+  void Drop(const std::vector<Evicted>& evict) {
+    if (evict.empty()) return;
+    for (const Evicted& e : evict) {
+      DeviceGuard g(e.device);
+      if (e.b.ready) (void)hipEventSynchronize(e.b.ready);
+      (void)hipFree(e.b.p);
+    }
+    std::lock_guard<std::mutex> l(mu_);
+    for (const Evicted& e : evict)
+      if (e.b.ready) events_[e.device].push_back(e.b.ready);
   }
   static size_t Bucket(size_t n) {
     if (n <= (size_t{1} << 20)) {

@@ -14,6 +14,11 @@ namespace dpf_amd {
 int SetError(int code, const std::string& message);
 const char* LastError();
 
+// Idle per-thread resource objects kept per kind (dpf_amd_set_thread_cache_cap).
+int ThreadCacheCap();
+// dpf_amd_set_force_peer_copies: cross-device copy branches on one device.
+bool ForcePeerCopies();
+
 // Device-side copy of dpf_amd_value_type plus everything the per-leaf
 // correction needs (kernel argument, < 2 KiB).
 constexpr int kMaxScalars = DPF_AMD_MAX_SCALARS;

@@ -148,6 +148,10 @@ StatusOr<std::unique_ptr<DenseDpfPirDatabase::Interface>> DenseDpfPirDatabase::B
     DPF_RETURN_IF_ERROR(HipStatus(hipGetDevice(&cur), "hipGetDevice"));
     devices.push_back(cur);
   }
+  for (int d : devices) DPF_RETURN_IF_ERROR(dpf_internal_host::CheckDevice(d));
+  if (device_records_ != nullptr)
+    DPF_RETURN_IF_ERROR(dpf_internal_host::CheckDevice(device_of_records_));
+  const bool force_peer = dpf_amd::ForcePeerCopies();
   const int64_t blocks = (n + 127) / 128;
   const int64_t num = static_cast<int64_t>(devices.size());
   for (int64_t g = 0; g < num; ++g) {
@@ -155,15 +159,21 @@ StatusOr<std::unique_ptr<DenseDpfPirDatabase::Interface>> DenseDpfPirDatabase::B
     const int64_t r1 = std::min(n, 128 * ShardBlock(blocks, g + 1, num));
     if (r1 > r0 || (g == 0 && n == 0)) db->shards_.push_back(Shard{devices[g], r0, r1, nullptr});
   }
-  for (const Shard& a : db->shards_)  // peer access for the partials' combine copies
-    for (const Shard& b : db->shards_)
-      if (a.device != b.device) {
-        dpf_internal_host::DeviceGuard g(a.device);
-        int can = 0;
-        if (hipDeviceCanAccessPeer(&can, a.device, b.device) == hipSuccess && can)
-          (void)hipDeviceEnablePeerAccess(b.device, 0);
-        (void)hipGetLastError();  // "already enabled" is not an error here
-      }
+  // Peer access between shard devices (the partials' combine copies) and
+  // from every shard device to the device holding the source rows (the
+  // build's row copies).
+  auto enable_peer = [](int from, int to) {
+    if (from == to) return;
+    dpf_internal_host::DeviceGuard g(from);
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, from, to) == hipSuccess && can)
+      (void)hipDeviceEnablePeerAccess(to, 0);
+    (void)hipGetLastError();  // "already enabled" is not an error here
+  };
+  for (const Shard& a : db->shards_) {
+    for (const Shard& b : db->shards_) enable_peer(a.device, b.device);
+    if (device_records_ != nullptr) enable_peer(a.device, device_of_records_);
+  }
   // Upload each shard in 64 MiB chunks of zero-padded fixed-stride rows.
   const int64_t rows_per_chunk = std::max<int64_t>(1, (64 << 20) / db->stride_);
   std::vector<char> chunk(rows_per_chunk * db->stride_);
@@ -193,15 +203,31 @@ StatusOr<std::unique_ptr<DenseDpfPirDatabase::Interface>> DenseDpfPirDatabase::B
       const char* src = static_cast<const char*>(device_records_) + sh.row_begin * fixed_size_;
       const int64_t rows = sh.row_end - sh.row_begin;
       if (rows == 0) continue;
-      if (fixed_size_ == db->stride_ && sh.device != device_of_records_)
+      const bool peer = sh.device != device_of_records_ || force_peer;
+      if (fixed_size_ == db->stride_ && peer) {
         DPF_RETURN_IF_ERROR(HipStatus(hipMemcpyPeer(sh.records, sh.device, src,
                                                     device_of_records_, rows * fixed_size_),
                                       "database peer copy"));
-      else
+      } else if (peer) {
+        // rows to re-stride on another device: one peer copy of the packed
+        // rows into the shard's device, then the strided copy there
+        void* packed = nullptr;
+        DPF_RETURN_IF_ERROR(MallocOrRelease(&packed, rows * fixed_size_));
+        Status cs = HipStatus(hipMemcpyPeer(packed, sh.device, src, device_of_records_,
+                                            rows * fixed_size_),
+                              "database peer copy");
+        if (cs.ok())
+          cs = HipStatus(hipMemcpy2D(sh.records, db->stride_, packed, fixed_size_, fixed_size_,
+                                     rows, hipMemcpyDeviceToDevice),
+                         "database device copy");
+        (void)hipFree(packed);
+        DPF_RETURN_IF_ERROR(cs);
+      } else {
         DPF_RETURN_IF_ERROR(HipStatus(
             hipMemcpy2D(sh.records, db->stride_, src, fixed_size_, fixed_size_, rows,
                         hipMemcpyDeviceToDevice),
             "database device copy"));
+      }
       continue;
     }
     for (int64_t r = sh.row_begin; r < sh.row_end; r += rows_per_chunk) {
@@ -371,7 +397,7 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
         char* dst = static_cast<char*>(gather) + g * part_bytes;
         st = HipStatus(hipStreamWaitEvent(s0, w[g].done, 0), "hipStreamWaitEvent");
         if (!st.ok()) break;
-        if (w[g].sh.device == dev0)
+        if (w[g].sh.device == dev0 && !dpf_amd::ForcePeerCopies())
           st = HipStatus(hipMemcpyAsync(dst, w[g].part, part_bytes, hipMemcpyDeviceToDevice, s0),
                          "partials copy");
         else

@@ -320,6 +320,23 @@ class DistributedPointFunction:
         out = out[:len(points)]
         return out if raw else vt.decode(out)
 
+    def evaluate_at_ctx(self, hierarchy_level: int, points: Sequence[int],
+                        ctx: EvaluationContext, value_type: ValueType = None,
+                        raw: bool = False):
+        """EvaluateAt<T>(hierarchy_level, points, ctx) (h:356-378): starts
+        from ctx's partial evaluations (from the root if it holds none) and
+        rewrites them at `hierarchy_level` (EvaluateAtImpl h:1000-1011)."""
+        vt = self._type(hierarchy_level, value_type)
+        tp = vt.to_proto()
+        pw = u128_words(_seq(points)) if len(points) else np.zeros(2, np.uint64)
+        out = np.zeros(max(len(points), 1), dtype=vt.numpy_dtype())
+        check(_lib.lib().dpf_amd_evaluate_at_ctx(self._h, hierarchy_level,
+                                                 pw.ctypes.data_as(ctypes.c_void_p), len(points),
+                                                 tp, len(tp), ctx._h,
+                                                 out.ctypes.data_as(ctypes.c_void_p)))
+        out = out[:len(points)]
+        return out if raw else vt.decode(out)
+
     def evaluate_and_apply(self, keys: Sequence[DpfKey], points: Sequence[int],
                            op: Callable[[list], bool], rightshift: int = 0,
                            value_type: ValueType = None):

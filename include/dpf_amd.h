@@ -87,6 +87,20 @@ const char* dpf_amd_version(void);
  * the bytes released to *released (may be NULL). */
 int dpf_amd_release_cached_memory(int64_t* released);
 
+/* Per-thread host resources (streams, pinned staging, incremental scratch)
+ * outlive their thread in a process-wide free list, so a server answering
+ * from short-lived threads creates them once per concurrent thread.  At most
+ * `cap` idle objects of each kind are kept (default 64, or
+ * DPF_AMD_THREAD_CACHE); the surplus is destroyed by the next thread that
+ * takes one, never in a thread-exit handler. */
+int dpf_amd_set_thread_cache_cap(int cap);
+
+/* Test hook (process-wide): 1 = a sharded DenseDpfPirDatabase takes the
+ * cross-device branches even between shards on one device (hipMemcpyPeer
+ * of the rows in Build, hipMemcpyPeerAsync of the partials in the combine),
+ * so one GPU executes the code an 8-GPU node runs.  0 = automatic. */
+void dpf_amd_set_force_peer_copies(int on);
+
 /* ------------------------------------------------------------------------ */
 /* Tier 1: device seams                                                     */
 /* ------------------------------------------------------------------------ */
@@ -380,6 +394,18 @@ int dpf_amd_evaluate_at(const dpf_amd_dpf* dpf, const uint8_t* key,
                         const uint64_t* points, int64_t num_points,
                         const uint8_t* value_type, size_t value_type_len,
                         void* out);
+
+/* EvaluateAt<T>(level, points, ctx) (h:356-378; EvaluateAtImpl h:1000-1011):
+ * starts from the partial evaluations stored in `ctx` (from the root when it
+ * holds none), walks them to `hierarchy_level`'s tree level, writes the
+ * num_points host-layout T values to `out`, and rewrites ctx's partial
+ * evaluations (the points' tree indices at `hierarchy_level`) and its
+ * previous_hierarchy_level.  Errors: the reference's, including "Prefix not
+ * present in ctx.partial_evaluations at hierarchy level <h>". */
+int dpf_amd_evaluate_at_ctx(const dpf_amd_dpf* dpf, int hierarchy_level,
+                            const uint64_t* points, int64_t num_points,
+                            const uint8_t* value_type, size_t value_type_len,
+                            dpf_amd_ctx* ctx, void* out);
 
 /* EvaluateAndApply<T, Fn> (h:403-407, 1072-1198): evaluates key i at point
  * i level by level, writing num_keys host-layout T values of level h to

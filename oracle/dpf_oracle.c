@@ -1530,6 +1530,66 @@ done:
   return st;
 }
 
+/* EvaluateAtImpl<T> with a context (h:356-378, 913-1070): the partial
+ * evaluations stored in `ctx` are walked to `h`'s tree level by
+ * ComputePartialEvaluations(tree_indices, h, update_ctx = true) (h:1000-1011),
+ * so no further levels remain (start_level = stop_level), then the seeds are
+ * hashed and corrected as without a context, and previous_hierarchy_level
+ * becomes h (h:1065-1067). */
+int or_evaluate_at_ctx(const or_dpf* d, int h, const uint64_t* point_words, int64_t n,
+                       or_ctx* ctx, uint64_t* out) {
+  if (h < 0) return set_err(OR_INVALID_ARGUMENT, "`hierarchy_level` must be non-negative");
+  if (h >= d->num_levels)
+    return set_err(OR_INVALID_ARGUMENT,
+                   "`hierarchy_level` must be less than the number of "
+                   "parameters passed at construction");
+  const or_key* key = ctx->key;
+  const u128* points = (const u128*)point_words;
+  int ld = d->log_domain[h];
+  u128 maxp = ~(u128)0;
+  if (ld < 128) maxp = ((u128)1 << ld) - 1;
+  for (int64_t i = 0; i < n; ++i)
+    if (points[i] > maxp)
+      return set_err(OR_INVALID_ARGUMENT,
+                     "`evaluation_points[%lld]` larger than the domain size at "
+                     "hierarchy level %d",
+                     (long long)i, h);
+  int st = validate_key(d, key);
+  if (st != OR_OK) return st;
+  if (n == 0) return OR_OK;
+  const vtype_t* vt = &d->vt[h];
+  int epb = vt->epb, ns = vt->num_scalars;
+  u128* tree = (u128*)malloc(sizeof(u128) * (size_t)n);
+  for (int64_t i = 0; i < n; ++i)
+    tree[i] = epb > 1 ? domain_to_tree_index(d, points[i], h) : points[i];
+  expansion_t sel = {0};
+  st = compute_partial_evaluations(d, tree, n, h, 1, ctx, &sel);
+  free(tree);
+  if (st != OR_OK) return st;
+  int bn = d->blocks_needed[h];
+  u128* hashed = hash_expanded_seeds(d, h, sel.seeds, n);
+  u128 corr[MAX_SCALARS * 16], cur[MAX_SCALARS * 16];
+  st = value_correction_array(d, key, h, corr);
+  if (st == OR_OK && hashed) {
+    for (int64_t i = 0; i < n; ++i) {
+      convert_bytes_to_array(vt, (const uint8_t*)(hashed + i * bn), 16 * bn, cur);
+      int bi = epb > 1 ? domain_to_block_index(d, points[i], h) : 0;
+      for (int s = 0; s < ns; ++s) {
+        u128 v = cur[bi * ns + s];
+        if (sel.cb[i]) v = s_add(&vt->scalars[s], v, corr[bi * ns + s]);
+        if (key->party == 1) v = s_neg(&vt->scalars[s], v);
+        store_u128(out + 2 * (i * ns + s), v);
+      }
+    }
+    ctx->previous_hierarchy_level = h;
+  } else if (st == OR_OK) {
+    st = set_err(OR_RESOURCE_EXHAUSTED, "Memory allocation error");
+  }
+  free(hashed);
+  expansion_free(&sel);
+  return st;
+}
+
 /* Subtree slice of the last hierarchy level (CPU baseline workload). */
 int or_expand_subtree(const or_dpf* d, const or_key* key, uint64_t first_lo,
                       uint64_t first_hi, int log_blocks, uint64_t* out) {

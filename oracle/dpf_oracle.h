@@ -144,6 +144,11 @@ int or_evaluate_until(const or_dpf* dpf, int hierarchy_level,
 int or_evaluate_at(const or_dpf* dpf, const or_key* key, int hierarchy_level,
                    const uint64_t* points, int64_t num_points, uint64_t* out);
 
+/* EvaluateAt<T>(level, points, ctx) (h:356-378, 1000-1011): starts from the
+ * partial evaluations in `ctx` and rewrites them at `hierarchy_level`. */
+int or_evaluate_at_ctx(const or_dpf* dpf, int hierarchy_level, const uint64_t* points,
+                       int64_t num_points, or_ctx* ctx, uint64_t* out);
+
 /* dpf_internal::EvaluateSeeds (evaluate_prg_hwy.cc:552-658): generic keys. */
 int or_evaluate_seeds(int64_t num_seeds, int num_levels,
                       int64_t num_correction_words, const uint64_t* seeds_in,

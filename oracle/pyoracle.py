@@ -94,6 +94,7 @@ def lib():
                                         ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
         L.or_evaluate_at.argtypes = [P, ctypes.POINTER(OrKey), ctypes.c_int, P,
                                      ctypes.c_int64, P]
+        L.or_evaluate_at_ctx.argtypes = [P, ctypes.c_int, P, ctypes.c_int64, P, P]
         L.or_evaluate_seeds.argtypes = [
             ctypes.c_int64, ctypes.c_int, ctypes.c_int64, P, P, P, ctypes.c_int,
             P, P, P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
@@ -477,6 +478,21 @@ class Dpf:
         out = np.zeros(max(2 * ns * len(points), 2), dtype=np.uint64)
         _check(lib().or_evaluate_at(self._h, key._p, level, _ptr(pw), len(points), _ptr(out)))
         return self._elements(out, ns, len(points))
+
+    def evaluate_at_ctx(self, level: int, points: Sequence[int], ctx: "Ctx"):
+        """EvaluateAt<T>(level, points, ctx) (h:356-378)."""
+        ns = num_scalars(self.levels[level][1])
+        return self._elements(self.evaluate_at_ctx_words(level, points, ctx).reshape(-1),
+                              ns, len(points))
+
+    def evaluate_at_ctx_words(self, level: int, points: Sequence[int], ctx: "Ctx"):
+        """As evaluate_at_ctx but returns the raw (n, ns, 2) uint64 words."""
+        ns = num_scalars(self.levels[level][1])
+        pw = u128_words(points) if len(points) else np.zeros(2, np.uint64)
+        n = len(points)
+        out = np.zeros(max(2 * ns * n, 2), dtype=np.uint64)
+        _check(lib().or_evaluate_at_ctx(self._h, level, _ptr(pw), n, ctx._h, _ptr(out)))
+        return out[:2 * ns * n].reshape(n, ns, 2)
 
     def evaluate_at_words(self, key: Key, level: int, points) -> np.ndarray:
         """As evaluate_at but returns the raw (n, ns, 2) uint64 words;

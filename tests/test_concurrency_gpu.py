@@ -171,3 +171,31 @@ def test_thread_resources_recycled_across_thread_generations(cuda):
     for _ in range(6):
         res = _run_threads(lambda t: work(t) == want[t % 3], 48)
         assert all(res)
+
+
+def test_thread_resource_cache_cap(cuda):
+    """With the idle-object cap at 4 (dpf_amd_set_thread_cache_cap), each
+    generation of 32 exiting threads parks 28 surplus objects of every kind,
+    which the next generation's first threads destroy (outside any
+    thread-exit handler) while the others evaluate; every result still
+    equals the single-threaded one."""
+    from distributed_point_functions_amd import _lib
+    from distributed_point_functions_amd import value_types as V
+    from distributed_point_functions_amd.dpf import DistributedPointFunction, DpfParameters
+    L = _lib.lib()
+    dpf = DistributedPointFunction.create_incremental(
+        [DpfParameters(ld, V.Integer(64)) for ld in (10, 16)])
+    k0, _ = dpf.generate_keys_incremental(4321, [1, 2], seeds=(41, 42))
+    p1 = list(range(1 << 10))
+
+    def work():
+        ctx = dpf.create_evaluation_context(k0)
+        return [dpf.evaluate_next(p, ctx, raw=True).tobytes() for p in ([], p1)]
+    want = work()
+    assert L.dpf_amd_set_thread_cache_cap(4) == 0
+    try:
+        for _ in range(4):
+            assert all(_run_threads(lambda t: work() == want, 32))
+    finally:
+        assert L.dpf_amd_set_thread_cache_cap(64) == 0
+    assert L.dpf_amd_set_thread_cache_cap(-1) == 3

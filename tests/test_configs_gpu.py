@@ -295,3 +295,43 @@ def test_c4_full_size_handle_request_on_sharded_database(c4_db):
     r1 = P.parse_response(s_plain.handle_request(req1))
     for i, a, b in zip(idx, r0, r1):
         assert bytes(x ^ y for x, y in zip(a, b)) == c4_db["host"][i].tobytes(), i
+
+
+def test_c4_full_size_forced_peer_copies_on_sharded_database(c4_db):
+    """The cross-device branches of the multi-GPU database forced on one GPU
+    (dpf_amd_set_force_peer_copies): hipMemcpyPeer of each shard's rows out
+    of the resident c4 tensor at build, hipMemcpyPeerAsync of the Q x 256 B
+    partials into the first shard's device before the fold
+    (pir/dense_dpf_pir_server.cc:92-127 spread over 8 shards).  Window scans
+    equal the oracle, HandleRequest equals the single-shard server, and the
+    parties' shares reconstruct the records."""
+    from distributed_point_functions_amd import _lib
+    from distributed_point_functions_amd import pir as P
+    from distributed_point_functions_amd import value_types as V
+    from distributed_point_functions_amd.dpf import DistributedPointFunction, DpfParameters
+    L = _lib.lib()
+    L.dpf_amd_set_force_peer_copies(1)
+    try:
+        sharded = P.DenseDpfPirDatabase([0] * 8).insert_fixed_device(c4_db["dev"], N4, REC).build()
+        assert len(sharded.shards()) == 8
+        sel = _window_selections(c4_db, 2, 2026)
+        lists = [[int(w[0]) | (int(w[1]) << 64) for w in sel[k]] for k in range(2)]
+        assert sharded.inner_product_with(lists) == _oracle_windows(c4_db, sel)
+        plain = P.DenseDpfPirDatabase()
+        plain.insert_fixed(c4_db["host"])
+        plain.build()
+        s_sharded = P.DenseDpfPirServer.create_plain(N4, sharded)
+        s_plain = P.DenseDpfPirServer.create_plain(N4, plain)
+        dpf = DistributedPointFunction.create(DpfParameters(26, V.XorWrapper(128)))
+        rng = random.Random(8026)
+        idx = [0, N4 - 1, (N4 // 8) - 1, N4 // 8] + [rng.randrange(N4) for _ in range(4)]
+        pairs = P.client_keys(dpf, N4, idx)
+        req0 = P.pir_request_plain([a for a, _ in pairs])
+        req1 = P.pir_request_plain([b for _, b in pairs])
+        r0 = P.parse_response(s_sharded.handle_request(req0))
+        assert r0 == P.parse_response(s_plain.handle_request(req0))
+        r1 = P.parse_response(s_sharded.handle_request(req1))
+        for i, a, b in zip(idx, r0, r1):
+            assert bytes(x ^ y for x, y in zip(a, b)) == c4_db["host"][i].tobytes(), i
+    finally:
+        L.dpf_amd_set_force_peer_copies(0)

@@ -1,0 +1,175 @@
+"""GPU parity of the incremental API paths the reference's IncrementalDpfTest
+drives (dpf/distributed_point_function_test.cc:308-930): EvaluateAt with a
+context (h:356-378, EvaluateAtImpl h:1000-1011) and EvaluateUntil calls that
+jump several hierarchy levels at once (level_step 2/3/5/7, h:695-891 walking
+hierarchy_to_tree[h] - hierarchy_to_tree[prev] levels from stored partial
+evaluations).
+
+Every instantiation of test.cc:698-930 runs through the C ABI
+(dpf_amd_evaluate_at_ctx / dpf_amd_evaluate_until) next to the CPU oracle:
+every output element of both parties, and the EvaluationContext each call
+leaves behind (previous_hierarchy_level, partial_evaluations_level and the
+ordered partial evaluations), must equal the oracle's; the reference's share
+sums are checked on top (tests/incremental_cases.py).
+"""
+import numpy as np
+import pytest
+
+from oracle import pyoracle as po
+from tests import incremental_cases as IC
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def api(cuda):
+    from distributed_point_functions_amd import dpf, value_types
+    return dpf, value_types
+
+
+def _make(api, levels):
+    D, V = api
+    params = [D.DpfParameters(ld, V.from_spec(s), sec) for ld, s, sec in levels]
+    return D.DistributedPointFunction.create_incremental(params)
+
+
+def _words(arr, bits):
+    """Host-layout output of a single-integer type -> (n, 2) {lo, hi}."""
+    f = arr["f0"]
+    if bits == 128:
+        return np.ascontiguousarray(f, dtype=np.uint64).reshape(-1, 2)
+    return np.stack([f.astype(np.uint64), np.zeros(len(f), np.uint64)], axis=1)
+
+
+def _same_ctx(ctx, octx):
+    assert ctx.previous_hierarchy_level == octx.previous_hierarchy_level
+    assert ctx.partial_evaluations_level == octx.partial_evaluations_level
+    got = ctx.partial_evaluations()
+    want = [(p, s, bool(c)) for p, s, c in octx.partial_evaluations()]
+    assert got == want
+
+
+def _evaluator(dpf, od, hier, ctxs, octxs):
+    def evaluate(h, prefixes, single_point):
+        bits = hier[h][1]
+        outs = []
+        for ctx, octx in zip(ctxs, octxs):
+            if single_point:
+                got = _words(dpf.evaluate_at_ctx(h, prefixes, ctx, raw=True), bits)
+                want = od.evaluate_at_ctx_words(h, prefixes, octx)[:, 0, :]
+            else:
+                got = _words(dpf.evaluate_until(h, prefixes, ctx, raw=True), bits)
+                want = od.evaluate_until_words(h, prefixes, octx)[:, 0, :]
+            assert got.shape == want.shape, h
+            bad = np.nonzero((got != want).any(axis=1))[0]
+            assert len(bad) == 0, (h, single_point, bad[:5])
+            _same_ctx(ctx, octx)
+            outs.append(got)
+        return outs
+    return evaluate
+
+
+@pytest.mark.parametrize("single_point", [False, True])
+@pytest.mark.parametrize("suite", IC.SUITES, ids=[s[0] for s in IC.SUITES])
+def test_incremental_dpf_correctness_vs_oracle(api, suite, single_point):
+    name, hier, alphas, betas_list, steps = suite
+    levels = IC.levels_of(hier)
+    dpf = _make(api, levels)
+    od = po.Dpf(levels)
+    for step in steps:
+        for alpha in alphas:
+            for betas in betas_list:
+                seeds = (alpha + 7, step)
+                keys = dpf.generate_keys_incremental(alpha, betas, seeds=seeds)
+                okeys = od.generate_keys(alpha, betas, seeds=seeds)
+                ctxs = [dpf.create_evaluation_context(k) for k in keys]
+                octxs = [od.create_evaluation_context(k) for k in okeys]
+                IC.run_case(hier, alpha, betas, step, single_point,
+                            _evaluator(dpf, od, hier, ctxs, octxs))
+
+
+def test_single_point_partial_evaluation_then_evaluate_until(api):
+    """test.cc:190-235: EvaluateAt(0, {prefix}, ctx) at a 108-bit level, then
+    EvaluateUntil(1, {prefix}, ctx) expands the 2^20 suffixes below it from
+    the stored partial evaluation — every output and context vs the oracle."""
+    levels = [(108, ("int", 32), 0), (128, ("int", 32), 0)]
+    dpf = _make(api, levels)
+    od = po.Dpf(levels)
+    prefix, suffix, beta = 0xdeadbeef, 23, 42
+    alpha = (prefix << 20) + suffix
+    keys = dpf.generate_keys_incremental(alpha, [beta, beta], seeds=(5, 6))
+    okeys = od.generate_keys(alpha, [beta, beta], seeds=(5, 6))
+    outs = []
+    for k, ok in zip(keys, okeys):
+        ctx, octx = dpf.create_evaluation_context(k), od.create_evaluation_context(ok)
+        a = _words(dpf.evaluate_at_ctx(0, [prefix], ctx, raw=True), 32)
+        assert np.array_equal(a, od.evaluate_at_ctx_words(0, [prefix], octx)[:, 0, :])
+        _same_ctx(ctx, octx)
+        u = _words(dpf.evaluate_until(1, [prefix], ctx, raw=True), 32)
+        assert np.array_equal(u, od.evaluate_until_words(1, [prefix], octx)[:, 0, :])
+        assert ctx.previous_hierarchy_level == octx.previous_hierarchy_level == 1
+        outs.append((a, u))
+    assert int(IC.share_sum(outs[0][0], outs[1][0], 32)[0, 0]) == beta
+    s = IC.share_sum(outs[0][1], outs[1][1], 32)
+    want = np.zeros_like(s)
+    want[suffix, 0] = beta
+    assert np.array_equal(s, want)
+
+
+def test_mixed_evaluate_until_and_evaluate_at_ctx(api):
+    """EvaluateUntil on level 0 and 1 (partial evaluations stored at level
+    0), then EvaluateAt with the context two levels further down (a walk of
+    the stored evaluations over several tree levels), then a level-skipping
+    EvaluateUntil from the points EvaluateAt stored; uint64 and uint128."""
+    for bits in (64, 128):
+        lds = [6, 12, 20, 33, 40]
+        levels = [(ld, ("int", bits), 0) for ld in lds]
+        dpf = _make(api, levels)
+        od = po.Dpf(levels)
+        rng = np.random.default_rng(bits)
+        alpha = int(rng.integers(0, 1 << 40))
+        betas = [11 + i for i in range(len(lds))]
+        keys = dpf.generate_keys_incremental(alpha, betas, seeds=(8, 9))
+        okeys = od.generate_keys(alpha, betas, seeds=(8, 9))
+        p1 = sorted({int(x) for x in rng.integers(0, 1 << 6, 20)} | {alpha >> 34})
+        low = [int(x) for x in rng.integers(0, 1 << 27, 300)]
+        pts3 = [(p1[i % len(p1)] << 27) | x for i, x in enumerate(low)] + [alpha >> 7]
+        outs = []
+        for k, ok in zip(keys, okeys):
+            ctx, octx = dpf.create_evaluation_context(k), od.create_evaluation_context(ok)
+            for h, pre in ((0, []), (1, p1)):
+                got = _words(dpf.evaluate_until(h, pre, ctx, raw=True), bits)
+                assert np.array_equal(got, od.evaluate_until_words(h, pre, octx)[:, 0, :])
+                _same_ctx(ctx, octx)
+            got = _words(dpf.evaluate_at_ctx(3, pts3, ctx, raw=True), bits)
+            assert np.array_equal(got, od.evaluate_at_ctx_words(3, pts3, octx)[:, 0, :])
+            _same_ctx(ctx, octx)
+            # 7 bits below every stored point, from the level-3 evaluations
+            got = _words(dpf.evaluate_until(4, pts3, ctx, raw=True), bits)
+            assert np.array_equal(got, od.evaluate_until_words(4, pts3, octx)[:, 0, :])
+            assert ctx.previous_hierarchy_level == 4
+            outs.append(got)
+        s = IC.share_sum(outs[0], outs[1], bits)
+        hit = len(pts3) - 1
+        assert int(s[hit * 128 + (alpha & 127), 0]) == betas[4]
+        s[hit * 128 + (alpha & 127)] = 0
+        assert not s.any()
+
+
+def test_evaluate_at_ctx_errors(api):
+    """The reference's errors through the ctx overload: a point outside the
+    domain, and a point whose prefix the context never evaluated."""
+    from distributed_point_functions_amd._lib import DpfAmdError
+    levels = [(4, ("int", 64), 0), (8, ("int", 64), 0)]
+    dpf = _make(api, levels)
+    k0, _ = dpf.generate_keys_incremental(3, [1, 2], seeds=(1, 2))
+    ctx = dpf.create_evaluation_context(k0)
+    dpf.evaluate_at_ctx(0, [1, 2], ctx)
+    with pytest.raises(DpfAmdError) as e:
+        dpf.evaluate_at_ctx(1, [0xff], ctx)
+    assert e.value.code == 3
+    assert "Prefix not present in ctx.partial_evaluations at hierarchy level 1" in str(e.value)
+    with pytest.raises(DpfAmdError) as e:
+        dpf.evaluate_at_ctx(1, [256], ctx)
+    assert "`evaluation_points[0]` larger than the domain size at hierarchy level 1" in str(e.value)
+    assert dpf.evaluate_at_ctx(1, [], ctx) == []

@@ -8,9 +8,15 @@ device — the reference's single InnerProductWith call
 (pir/dense_dpf_pir_server.cc:92-127, pir/pir_database_interface.h:65-66)
 spread over GPUs.  ExpandLeavesOnDevices splits one key's domain the same
 way (c5).  With devices {0, 0, ...} every shard runs on this GPU through the
-same code path (per-device streams, peer-copy branch for same-device
-partials, fold), and the results must equal the single-shard library and the
-oracle bit for bit.
+same code path (per-device streams, the partials' combine, the fold), and
+the results must equal the single-shard library and the oracle bit for bit.
+Shards on one device take the device-local copy branches by default; the
+`forced_peer` tests turn on dpf_amd_set_force_peer_copies so the
+cross-device branches (hipMemcpyPeer of rows at build — packed, then
+re-strided for record sizes that are not a multiple of 16 —, and
+hipMemcpyPeerAsync of the partials) execute here too.  Two distinct GPUs
+are exercised only when the box has them (test_two_devices_*); the 8-GPU
+node is the driver's.
 """
 import random
 
@@ -155,3 +161,78 @@ def test_insert_fixed_device_equals_host_built(P, cuda, size, shards):
     rng = random.Random(size)
     sels = _sel(rng, 6, n)
     assert dev_db.inner_product_with(sels) == host_db.inner_product_with(sels)
+
+
+@pytest.fixture
+def forced_peer(P):
+    from distributed_point_functions_amd import _lib
+    L = _lib.lib()
+    L.dpf_amd_set_force_peer_copies(1)
+    yield
+    L.dpf_amd_set_force_peer_copies(0)
+
+
+@pytest.mark.parametrize("n,size,q,shards", [(1000, 240, 5, 4), (128 * 37 + 5, 256, 20, 3),
+                                             (300, 16, 3, 5), (4096, 1040, 2, 2)])
+def test_forced_peer_inner_product_matches_oracle(P, forced_peer, n, size, q, shards):
+    rng = random.Random(n * 11 + q)
+    recs = np.random.default_rng(n * 3 + q).integers(0, 256, (n, size), dtype=np.uint8)
+    db = _db(P, recs, [0] * shards)
+    sels = _sel(rng, q, n)
+    rows = [recs[i].tobytes() for i in range(n)]
+    assert db.inner_product_with(sels) == po.inner_product(rows, sels)
+
+
+@pytest.mark.parametrize("size,shards", [(256, [0, 0, 0]), (40, [0, 0, 0]), (1040, [0, 0])])
+def test_forced_peer_device_rows_build(P, cuda, forced_peer, size, shards):
+    """Rows in HBM copied to each shard by hipMemcpyPeer (40 B rows: one peer
+    copy of the packed rows, then the 48 B re-stride on the shard device)."""
+    import torch
+    n = 128 * 21 + 9
+    g = torch.Generator(device=cuda)
+    g.manual_seed(size + 1)
+    rows = torch.randint(0, 256, (n * size,), dtype=torch.uint8, device=cuda, generator=g)
+    dev_db = P.DenseDpfPirDatabase(shards).insert_fixed_device(rows, n, size).build()
+    host = rows.cpu().numpy().reshape(n, size)
+    rng = random.Random(size + 1)
+    sels = _sel(rng, 6, n)
+    assert dev_db.inner_product_with(sels) == po.inner_product(
+        [host[i].tobytes() for i in range(n)], sels)
+
+
+def test_invalid_device_ids_are_rejected(cuda):
+    """ExpandLeavesOnDevices checks every device id before any launch."""
+    import torch
+    from distributed_point_functions_amd import _lib
+    from distributed_point_functions_amd import value_types as V
+    from distributed_point_functions_amd.dpf import DistributedPointFunction, DpfParameters
+    dpf = DistributedPointFunction.create(DpfParameters(12, V.Integer(64)))
+    k0, _ = dpf.generate_keys(5, 6)
+    out = torch.empty(4096 * 8, dtype=torch.uint8, device=cuda)
+    with pytest.raises(_lib.DpfAmdError) as e:
+        dpf.expand_leaves_on_devices(k0, [(0, 0, 1024, out), (1 << 20, 1024, 2048, out)])
+    assert e.value.code == 3 and "invalid device id" in e.value.message
+
+
+@pytest.mark.skipif("not __import__('torch').cuda.is_available() or "
+                    "__import__('torch').cuda.device_count() < 2",
+                    reason="needs two GPUs")
+def test_two_devices_sharded_inner_product_and_expansion(P):
+    import torch
+    n, size, q = 128 * 40 + 3, 240, 7
+    recs = np.random.default_rng(2).integers(0, 256, (n, size), dtype=np.uint8)
+    rng = random.Random(2)
+    sels = _sel(rng, q, n)
+    assert _db(P, recs, [0, 1]).inner_product_with(sels) == _db(P, recs).inner_product_with(sels)
+    from distributed_point_functions_amd import value_types as V
+    from distributed_point_functions_amd.dpf import DistributedPointFunction, DpfParameters
+    dpf = DistributedPointFunction.create(DpfParameters(20, V.Integer(64)))
+    k0, _ = dpf.generate_keys(12345, 6, seeds=(1, 2))
+    nt = 1 << dpf.hierarchy_to_tree(0)  # tree leaves, two uint64 elements each
+    half = nt // 2
+    a = torch.empty(half * 16, dtype=torch.uint8, device="cuda:0")
+    b = torch.empty(half * 16, dtype=torch.uint8, device="cuda:1")
+    full = torch.empty(nt * 16, dtype=torch.uint8, device="cuda:0")
+    dpf.expand_leaves_on_devices(k0, [(0, 0, half, a), (1, half, nt, b)])
+    dpf.expand_leaves_on_devices(k0, [(0, 0, nt, full)])
+    assert torch.equal(torch.cat([a, b.to("cuda:0")]), full)
