@@ -425,6 +425,132 @@ def cpu_baseline(args):
     return out
 
 
+# --- the reference's published experiments (experiments/README.md:20-108) ---
+
+EXPERIMENT_PUBLISHED_S = {  # one key, 1 thread of a 2.3 GHz Xeon (README tables)
+    (32, "hierarchical"): {"0.1": 1.36, "0.5": 2.22, "uniform": 3.31},
+    (32, "direct"): {"0.1": 0.67, "0.5": 0.68, "uniform": 0.70},
+    (128, "hierarchical"): {"0.1": 32.68, "0.5": 35.07, "uniform": 35.95},
+    (128, "direct"): {"0.1": 3.08, "0.5": 3.13, "uniform": 3.13},
+}
+
+
+def experiment_nonzeros(log_domain, dist, n=1 << 20, seed=2021):
+    """2^20 distinct non-zero buckets in [0, 2^log_domain), sorted, as an (n,
+    2) uint64 {lo, hi} array.  The reference's CSV inputs are git-LFS
+    pointers (absent), so the README's three distributions (README:8-15) are
+    drawn here: "power law with 90 % of non-zeros in a fraction f of the
+    domain" as x = floor(2^B u^a) with u uniform and a = ln f / ln 0.9 (so
+    P(x < f 2^B) = 0.9), and uniform (a = 1); duplicates are redrawn."""
+    import math
+    rng = np.random.default_rng(seed + 7 * log_domain + {"0.1": 1, "0.5": 2, "uniform": 3}[dist])
+    a = 1.0 if dist == "uniform" else math.log(float(dist)) / math.log(0.9)
+    have = np.zeros((0, 2), dtype=np.uint64)  # (hi, lo) rows
+    while len(have) < n:
+        m = int((n - len(have)) * 1.5) + 1024
+        v = rng.random(m) ** a
+        if log_domain <= 53:
+            hi = np.zeros(m, np.uint64)
+            lo = np.floor(v * float(1 << log_domain)).astype(np.uint64)
+        else:  # 53 bits from v, the rest uniform below them
+            top = (v * float(1 << 53)).astype(np.uint64)
+            r_lo = rng.integers(0, 1 << 63, m, dtype=np.uint64) * 2 + rng.integers(0, 2, m, dtype=np.uint64)
+            sh = log_domain - 53  # bits below the 53 drawn ones
+            if sh >= 64:
+                r_hi = rng.integers(0, 1 << (sh - 64), m, dtype=np.uint64) if sh > 64 else np.zeros(m, np.uint64)
+                hi = (top << np.uint64(sh - 64)) | r_hi
+                lo = r_lo
+            else:
+                lo = (r_lo & np.uint64((1 << sh) - 1)) | (top << np.uint64(sh))
+                hi = top >> np.uint64(64 - sh) if sh else np.zeros(m, np.uint64)
+        have = np.unique(np.concatenate([have, np.stack([hi, lo], axis=1)]), axis=0)
+    keep = np.sort(rng.choice(len(have), n, replace=False))
+    hl = have[keep]
+    return np.ascontiguousarray(np.stack([hl[:, 1], hl[:, 0]], axis=1))
+
+
+def _shift_unique(lohi, s):
+    """Sorted unique (n, 2) {lo, hi} words of x >> s (ComputePrefixes,
+    experiments/synthetic_data_benchmarks.cc:100-121)."""
+    lo, hi = lohi[:, 0], lohi[:, 1]
+    if s >= 128:
+        return np.zeros((1, 2), np.uint64)
+    if s >= 64:
+        lo, hi = hi >> np.uint64(s - 64), np.zeros_like(hi)
+    elif s > 0:
+        lo, hi = (lo >> np.uint64(s)) | (hi << np.uint64(64 - s)), hi >> np.uint64(s)
+    keep = np.ones(len(lo), bool)
+    keep[1:] = (lo[1:] != lo[:-1]) | (hi[1:] != hi[:-1])  # input sorted: runs of equals
+    return np.ascontiguousarray(np.stack([lo[keep], hi[keep]], axis=1))
+
+
+def _oracle_experiment(log_domain, lohi):
+    """The oracle (1 core) on the same workload, one iteration of each mode:
+    hierarchical over the README levels (prefixes prepared outside the timed
+    region, as the reference's benchmark does), then EvaluateAt at the
+    non-zeros."""
+    from oracle import pyoracle as po
+    levels = list(range(21, log_domain, 2)) + [log_domain]
+    pre = [None] + [_shift_unique(lohi, log_domain - levels[i - 1]) for i in range(1, len(levels))]
+    od = po.Dpf([(ld, ("int", 32), 0) for ld in levels])
+    alpha = int(lohi[len(lohi) // 3, 0]) | (int(lohi[len(lohi) // 3, 1]) << 64)
+    k0, _ = od.generate_keys(alpha, [1] * len(levels), seeds=(5, 6))
+    ctx = od.create_evaluation_context(k0)
+    t0 = time.perf_counter()
+    for i in range(len(levels)):
+        od.evaluate_until_words(i, [] if i == 0 else pre[i], ctx)
+    hier = time.perf_counter() - t0
+    d1 = po.Dpf([(log_domain, ("int", 32), 0)])
+    k1, _ = d1.generate_keys(alpha, [1], seeds=(7, 8))
+    t0 = time.perf_counter()
+    d1.evaluate_at_words(k1, 0, lohi)
+    direct = time.perf_counter() - t0
+    return hier, direct
+
+
+def main_experiments(args):
+    """bench.py --experiments: the reference's published workloads through the
+    C++ API (tools/experiments_bench.cc, GPU) with the oracle on one host
+    core beside them; one JSON line per case and a summary line."""
+    import subprocess
+    import tempfile
+    exe = os.path.join(os.path.dirname(_lib.LIB_PATH), "experiments_bench")
+    rows = []
+    for log_domain in (32, 128):
+        for dist in ("0.1", "0.5", "uniform"):
+            nz = experiment_nonzeros(log_domain, dist)
+            with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+                nz.tofile(f)
+                path = f.name
+            try:
+                out = subprocess.run([exe, path, str(log_domain), str(args.steps), dist],
+                                     capture_output=True, text=True, timeout=900)
+            finally:
+                os.unlink(path)
+            if out.returncode != 0:
+                raise RuntimeError("experiments_bench failed: " + out.stderr[-2000:])
+            gpu = {json.loads(l)["workload"]: json.loads(l) for l in out.stdout.splitlines()
+                   if l.startswith("{")}
+            cpu = None
+            if not args.skip_cpu_baseline and (log_domain == 32 or dist == "uniform"):
+                h, d = _oracle_experiment(log_domain, nz)
+                cpu = {"hierarchical": h, "direct": d}
+            for mode in ("hierarchical", "direct"):
+                g = gpu[mode]
+                row = dict(g)
+                row["published_reference_s"] = EXPERIMENT_PUBLISHED_S[(log_domain, mode)][dist]
+                row["speedup_vs_published"] = row["published_reference_s"] / g["best_s"]
+                if cpu:
+                    row["cpu_baseline"] = {"value_s": cpu[mode], "cores": 1, "kind": "port",
+                                           "sample": "oracle/dpf_oracle.c, same non-zeros, "
+                                                     "one iteration"}
+                rows.append(row)
+                print(json.dumps(row), flush=True)
+    print(json.dumps({"experiments": "experiments/README.md:20-108 workloads, synthetic non-zeros",
+                      "cases": len(rows),
+                      "all_correct": all(r.get("correct") for r in rows)}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -442,10 +568,15 @@ def main():
     ap.add_argument("--force-peer", action="store_true",
                     help="--in-process: take the cross-device copy branches even between "
                          "slices on one device (dpf_amd_set_force_peer_copies)")
+    ap.add_argument("--experiments", action="store_true",
+                    help="time the reference's published experiment workloads (one key, 2^20 "
+                         "non-zeros, domains 2^32 / 2^128) through the C++ API instead")
     ap.add_argument("--in-process", action="store_true",
                     help="drive all --gpus GPUs from this one process through the library's "
                          "multi-GPU API (ExpandLeavesOnDevices, a sharded DenseDpfPirDatabase)")
     args = ap.parse_args()
+    if args.experiments:
+        return main_experiments(args)
     if args.in_process:
         if args.force_peer:
             _lib.lib().dpf_amd_set_force_peer_copies(1)

@@ -113,6 +113,7 @@ def lib():
     _sig(L, "dpf_amd_set_scan_m4", I32, I32)
     _sig(L, "dpf_amd_set_walk_mode", I32, I32)
     _sig(L, "dpf_amd_set_dcf_kernel", I32, I32)
+    _sig(L, "dpf_amd_set_prefix_expand", I32, I32)
     _bind_tier2(L)
     _lib = L
     return L

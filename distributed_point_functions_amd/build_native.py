@@ -24,6 +24,10 @@ CPP_TEST = os.path.join(OUT_DIR, "cpp_api_test")
 # C++ API wall-clock bench of the BASELINE configs c1-c3 (tools/cpp_api_bench.cc).
 CPP_BENCH_SRC = os.path.join(ROOT, "tools", "cpp_api_bench.cc")
 CPP_BENCH = os.path.join(OUT_DIR, "cpp_api_bench")
+# The reference's published experiment workloads through the C++ API
+# (tools/experiments_bench.cc; driven by bench.py --experiments).
+EXP_BENCH_SRC = os.path.join(ROOT, "tools", "experiments_bench.cc")
+EXP_BENCH = os.path.join(OUT_DIR, "experiments_bench")
 ARCH = os.environ.get("DPF_AMD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -95,7 +99,8 @@ def build(force: bool = False, jobs: int = 8) -> str:
         subprocess.check_call(["hipcc", "--offload-arch=" + ARCH, "-shared", "-fPIC",
                                "-o", tmp] + objs + ["-lpthread"])
         os.replace(tmp, LIB)
-    for src, exe in ((CPP_TEST_SRC, CPP_TEST), (CPP_BENCH_SRC, CPP_BENCH)):
+    for src, exe in ((CPP_TEST_SRC, CPP_TEST), (CPP_BENCH_SRC, CPP_BENCH),
+                     (EXP_BENCH_SRC, EXP_BENCH)):
         if os.path.exists(src) and (
                 force or not os.path.exists(exe) or
                 os.path.getmtime(exe) < max(os.path.getmtime(LIB), os.path.getmtime(src),

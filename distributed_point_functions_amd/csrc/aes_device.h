@@ -378,6 +378,123 @@ __device__ __forceinline__ void QuadWalkStep(uint32_t& x, uint32_t& t, uint32_t 
   if (c == 0) x &= ~1u;
 }
 
+// ---- latency-bound quad walks (KEvaluatePointsQuad) -------------------------
+//
+// A quad round is a dependent chain: 3 DPP moves -> 4 v_perm -> 4 ds_read_b32
+// -> the combine -> the next round, at one wave per SIMD (one key's 16,384-
+// point EvaluateAt).  Two cuts of the chain's post-lookup part:
+//  * the per-lane left/right key choice is folded into the round keys once
+//    per level (rk ^ (diff & m), off the chain) instead of an XOR after every
+//    round (DPF_QUAD_RKM);
+//  * four tables instead of two (DPF_QUAD_T4): T2 = rotl16(T0) and T3 =
+//    rotl16(T1) stored in a second 64 KiB half (128 KiB per block), so the
+//    combine is Xor3(t0, t1, Xor3(t2, t3, rk)) without the rotl16.  The upper
+//    half's address comes from the same single v_perm: its lane-offset source
+//    carries 0x01 in byte 2 (address bit 16).
+#ifndef DPF_QUAD_RKM
+#define DPF_QUAD_RKM 1
+#endif
+constexpr int kTab4Words = 2 * kTabWords;  // 128 KiB
+
+__device__ __forceinline__ void FillTables4(uint32_t* tab) {
+  for (int i = threadIdx.x; i < kTab4Words; i += blockDim.x) {
+    const int j = i & (kTabWords - 1);
+    uint32_t v = c_te0.t[j >> 6];
+    if (j & 32) v = (v << 8) | (v >> 24);      // T1 = rotl8(T0)
+    if (i >= kTabWords) v = (v << 16) | (v >> 16);  // T2 / T3 = rotl16(T0 / T1)
+    tab[i] = v;
+  }
+}
+
+struct Lds4 {
+  const char* base;
+  uint32_t laneoff;     // (lane & 31) * 4
+  uint32_t laneoff_hi;  // laneoff | 0x10000: the [T2 | T3] half
+};
+__device__ __forceinline__ Lds4 MakeLds4(const uint32_t* tab) {
+  const uint32_t lo = (threadIdx.x & 31u) * 4u;
+  return Lds4{reinterpret_cast<const char*>(tab), lo, lo | 0x10000u};
+}
+// byte k of x -> address bits 8..15, byte 2 of the lane-offset source -> bits 16..23
+#define DPF_SEL_HI(k) (0x0c020000u | ((4u + (k)) << 8))
+__device__ __forceinline__ uint32_t LoadT2(const Lds4& L, uint32_t x, int k) {
+  const uint32_t a = __builtin_amdgcn_perm(x, L.laneoff_hi, DPF_SEL_HI(k));
+  return *reinterpret_cast<const uint32_t*>(L.base + a);
+}
+__device__ __forceinline__ uint32_t LoadT3(const Lds4& L, uint32_t x, int k) {
+  const uint32_t a = __builtin_amdgcn_perm(x, L.laneoff_hi, DPF_SEL_HI(k));
+  return *reinterpret_cast<const uint32_t*>(L.base + a + 128);
+}
+
+__device__ __forceinline__ Lds LdsOf(const Lds& L) { return L; }
+__device__ __forceinline__ Lds LdsOf(const Lds4& L) { return Lds{L.base, L.laneoff}; }
+
+// Column c's plain round-key words of DPF key W (rounds 0..10).
+struct QuadRk {
+  uint32_t rk[11];
+};
+template <int W>
+__device__ __forceinline__ QuadRk MakeQuadRk(int c) {
+  QuadRk k;
+#pragma unroll
+  for (int r = 0; r < 11; ++r)
+    k.rk[r] = PickCol(c, kDpfKeys[W].rk[4 * r], kDpfKeys[W].rk[4 * r + 1],
+                      kDpfKeys[W].rk[4 * r + 2], kDpfKeys[W].rk[4 * r + 3]);
+  return k;
+}
+// The level's round keys of this lane: left key, or right where m = ~0.
+__device__ __forceinline__ QuadRk MaskQuadRk(const QuadRk& kl, const QuadDiff& d, uint32_t m) {
+  QuadRk k;
+#pragma unroll
+  for (int r = 0; r < 11; ++r) k.rk[r] = kl.rk[r] ^ (d.d[r] & m);
+  return k;
+}
+
+// AES-128 of the quad's state with per-lane round keys `k` (plain words).
+// T4: four tables (Lds4); otherwise T0/T1 with the rotl16 in the combine.
+template <bool T4, class LT>
+__device__ __forceinline__ uint32_t AesQuadRk(uint32_t w, const QuadRk& k, const LT& L) {
+  w ^= k.rk[0];
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    const uint32_t x1 = QuadPerm<kQuadNext1>(w), x2 = QuadPerm<kQuadNext2>(w),
+                   x3 = QuadPerm<kQuadNext3>(w);
+    if constexpr (T4) {
+      const uint32_t t0 = LoadT0(LdsOf(L), w, 0),
+                     t1 = LoadT1(LdsOf(L), x1, 1), t2 = LoadT2(L, x2, 2),
+                     t3 = LoadT3(L, x3, 3);
+      w = Xor3(t0, t1, Xor3(t2, t3, k.rk[r]));
+    } else {
+      const uint32_t t0 = LoadT0(L, w, 0), t1 = LoadT1(L, x1, 1), t2 = LoadT0(L, x2, 2),
+                     t3 = LoadT1(L, x3, 3);
+      // rotl16(t2 ^ t3 ^ rotr16(rk)) = rotl16(t2 ^ t3) ^ rk
+      w = Xor3(t0, t1, Rotl16(Xor3(t2, t3, __builtin_amdgcn_alignbit(k.rk[r], k.rk[r], 16))));
+    }
+  }
+  const Lds L2 = LdsOf(L);
+  const uint32_t x1 = QuadPerm<kQuadNext1>(w), x2 = QuadPerm<kQuadNext2>(w),
+                 x3 = QuadPerm<kQuadNext3>(w);
+  const uint32_t t0 = LoadT0(L2, w, 0), t1 = LoadT0(L2, x1, 1), t2 = LoadT0(L2, x2, 2),
+                 t3 = LoadT1(L2, x3, 3);
+  const uint32_t lo = __builtin_amdgcn_perm(t1, t0, 0x0c0c0501u);
+  const uint32_t hi = __builtin_amdgcn_perm(t3, t2, 0x07020c0cu);
+  return Xor3(lo, hi, k.rk[10]);
+}
+
+// QuadWalkStep with the level's keys folded once (rk ^ (diff & m)).
+template <bool T4, class LT>
+__device__ __forceinline__ void QuadWalkStepRk(uint32_t& x, uint32_t& t, uint32_t bit,
+                                               uint32_t cw_word, uint32_t cl, uint32_t cr, int c,
+                                               const QuadRk& kl, const QuadDiff& kd,
+                                               const LT& L) {
+  const QuadRk k = MaskQuadRk(kl, kd, 0u - bit);
+  const uint32_t sg = SigmaQuad(x, c);
+  const uint32_t st = AesQuadRk<T4>(sg, k, L);
+  x = st ^ sg ^ (cw_word & (0u - t));
+  const uint32_t lsb = QuadPerm<kQuadBcast<0>>(x) & 1u;
+  t = lsb ^ (t & (bit ? cr : cl));
+  if (c == 0) x &= ~1u;
+}
 
 __device__ __forceinline__ u128 ToU128(const uint32_t (&x)[4]) {
   return (u128)x[0] | ((u128)x[1] << 32) | ((u128)x[2] << 64) | ((u128)x[3] << 96);

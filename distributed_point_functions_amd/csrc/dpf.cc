@@ -1423,6 +1423,16 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   // outputs of one tree index = 2^bbits prefixes x outputs_per_prefix, so
   // every offset below is in range by construction
   const int64_t seg = (int64_t{1} << levels) * cepb;
+  // Per-prefix expansion (default; dpf_amd_set_prefix_expand): a prefix p of
+  // the previous level is itself a tree node, at depth previous_log_domain_size;
+  // when this level's tree level is not above it, expanding p's subtree gives
+  // exactly p's outputs_per_prefix outputs, in prefix order.  The roots are
+  // the partial evaluations of p's tree index walked down p's last bbits
+  // bits, so no sibling subtree is expanded, no staging buffer is written and
+  // no gather runs (c3: 2^16 prefixes, half the AES and none of the 256 MiB
+  // staging round trip).  `src` then holds each prefix's unique-root index.
+  const bool fused = !dpf_amd::PrefixExpandOff() && !prefixes.empty() &&
+                     stop_level >= previous_log_domain_size;
   if (!prefixes.empty()) {
     const int bbits = st.parameters[prev_h].log_domain_size() - st.hierarchy_to_tree[prev_h];
     const uint64_t bmask = (uint64_t{1} << bbits) - 1;  // bbits <= 7 (epb <= 128)
@@ -1457,9 +1467,10 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
         for (int64_t i = b; i < e; ++i) {
           const uint128 t = prefixes[i] >> bbits;
           if (i == 0 || t != (prefixes[i - 1] >> bbits)) tree_indices[u++] = t;
-          src[i] = (u - 1) * seg +
-                   static_cast<int64_t>(static_cast<uint64_t>(prefixes[i]) & bmask) *
-                       outputs_per_prefix;
+          src[i] = fused ? u - 1
+                         : (u - 1) * seg +
+                               static_cast<int64_t>(static_cast<uint64_t>(prefixes[i]) & bmask) *
+                                   outputs_per_prefix;
         }
       });
     } else {
@@ -1470,9 +1481,10 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
         const uint128 ti = prefixes[i] >> bbits;
         auto it = inverse.emplace(ti, num_unique);
         if (it.second) tree_indices[num_unique++] = ti;
-        src[i] = it.first->second * seg +
-                 static_cast<int64_t>(static_cast<uint64_t>(prefixes[i]) & bmask) *
-                     outputs_per_prefix;
+        src[i] = fused ? it.first->second
+                       : it.first->second * seg +
+                             static_cast<int64_t>(static_cast<uint64_t>(prefixes[i]) & bmask) *
+                                 outputs_per_prefix;
       }
     }
   }
@@ -1500,6 +1512,66 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
         ctx, s, &roots, &root_seeds, &root_cb, &pending));
   }
   trace.Mark("partial_evaluations");
+  if (fused) {
+    const int prev_tree = st.hierarchy_to_tree[prev_h];
+    const int walk = previous_log_domain_size - prev_tree;  // p's bits below its tree index
+    const int down = stop_level - previous_log_domain_size;
+    const size_t stride = static_cast<size_t>(vt.out_stride);
+    CwArrays wc = KeyCws(ctx.key(), prev_tree, previous_log_domain_size);
+    CwArrays ec = KeyCws(ctx.key(), previous_log_domain_size, stop_level);
+    using Part = UploadRing::HostPart;
+    // every input in one packed upload: root index per prefix, the prefixes
+    // (the walk's paths), both correction-word ranges
+    const Part parts[8] = {{src.data(), size_t(8) * num_prefixes},
+                           {prefixes.data(), walk ? size_t(16) * num_prefixes : 0},
+                           {wc.seeds.data(), size_t(16) * walk},
+                           {wc.ccl.data(), size_t(walk)},
+                           {wc.ccr.data(), size_t(walk)},
+                           {ec.seeds.data(), size_t(16) * down},
+                           {ec.ccl.data(), size_t(down)},
+                           {ec.ccr.data(), size_t(down)}};
+    size_t off[8];
+    const size_t in_bytes = UploadRing::PackedLayout(parts, 8, off);
+    const size_t seeds_off = in_bytes;
+    const size_t cb_off = seeds_off + size_t(16) * num_prefixes;
+    DeviceBuffer work, result;
+    DPF_RETURN_IF_ERROR(work.Alloc(cb_off + num_prefixes, s));
+    char* d = work.as<char>();
+    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 8, in_bytes, off, s));
+    void* pseeds = d + seeds_off;
+    uint8_t* pcb = reinterpret_cast<uint8_t*>(d + cb_off);
+    DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd::GatherRoots(
+        num_prefixes, reinterpret_cast<const int64_t*>(d + off[0]), num_unique, root_seeds, root_cb,
+        pseeds, pcb, s)));
+    if (walk > 0)
+      DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_seeds(
+          num_prefixes, walk, walk, pseeds, pcb, d + off[1], 0, d + off[2],
+          reinterpret_cast<const uint8_t*>(d + off[3]), reinterpret_cast<const uint8_t*>(d + off[4]),
+          dpf_amd::kPrgKeyLeftLo, dpf_amd::kPrgKeyLeftHi, dpf_amd::kPrgKeyRightLo,
+          dpf_amd::kPrgKeyRightHi, pseeds, pcb, s)));
+    void* final_dev = out;
+    if (!out_on_device) {
+      DPF_RETURN_IF_ERROR(result.Alloc(total * stride, s));
+      final_dev = result.get();
+    }
+    DPF_RETURN_IF_ERROR(ClearPadding(vt, final_dev, total * stride, s));
+    DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_expand_and_correct(
+        num_prefixes, pseeds, pcb, down, d + off[5], reinterpret_cast<const uint8_t*>(d + off[6]),
+        reinterpret_cast<const uint8_t*>(d + off[7]), &vt,
+        reinterpret_cast<const uint64_t*>(corr.data()), ctx.key().party(), cepb, 0,
+        num_prefixes << down, final_dev, s)));
+    trace.Mark("prefix_expand_launch");
+    // the context rewrite runs while the expansion does
+    DPF_RETURN_IF_ERROR(FinishContextUpdate(pending, ctx));
+    trace.Mark("ctx_rewrite");
+    if (!out_on_device)
+      DPF_RETURN_IF_ERROR(CopyToHostSync(out, final_dev, total * stride, s));
+    else
+      DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+    trace.Mark("copy+sync");
+    ctx.set_previous_hierarchy_level(hierarchy_level);
+    return OkStatus();
+  }
   CwArrays cw = KeyCws(ctx.key(), start_level, stop_level);
   DeviceBuffer cws, ccl, ccr;
   DPF_RETURN_IF_ERROR(cws.Upload(cw.seeds.data(), 16 * levels, s));

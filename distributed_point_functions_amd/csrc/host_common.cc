@@ -92,10 +92,18 @@ std::atomic<int> g_thread_cache_cap{[] {
   return e ? atoi(e) : 64;
 }()};
 std::atomic<int> g_force_peer_copies{0};
+thread_local int t_prefix_expand = 0;  // 0 automatic, 1 off
 }  // namespace
 
 int ThreadCacheCap() { return g_thread_cache_cap.load(std::memory_order_relaxed); }
 bool ForcePeerCopies() { return g_force_peer_copies.load(std::memory_order_relaxed) != 0; }
+bool PrefixExpandOff() {
+  static const bool env_off = [] {
+    const char* e = getenv("DPF_AMD_PREFIX_EXPAND");
+    return e && atoi(e) == 0;
+  }();
+  return env_off || t_prefix_expand == 1;
+}
 
 }  // namespace dpf_amd
 
@@ -112,5 +120,12 @@ int dpf_amd_set_thread_cache_cap(int cap) {
 }
 
 void dpf_amd_set_force_peer_copies(int on) { dpf_amd::g_force_peer_copies.store(on ? 1 : 0); }
+
+int dpf_amd_set_prefix_expand(int mode) {
+  if (mode < 0 || mode > 1) return -2;
+  const int prev = dpf_amd::t_prefix_expand;
+  dpf_amd::t_prefix_expand = mode;
+  return prev;
+}
 
 }  // extern "C"

@@ -18,6 +18,9 @@ const char* LastError();
 int ThreadCacheCap();
 // dpf_amd_set_force_peer_copies: cross-device copy branches on one device.
 bool ForcePeerCopies();
+// dpf_amd_set_prefix_expand / DPF_AMD_PREFIX_EXPAND=0: EvaluateUntil expands
+// unique tree indices and gathers, instead of expanding per prefix.
+bool PrefixExpandOff();
 
 // Device-side copy of dpf_amd_value_type plus everything the per-leaf
 // correction needs (kernel argument, < 2 KiB).
@@ -96,5 +99,11 @@ int EvaluatePointsIndexed(int64_t num_points, const int32_t* key_index, int64_t 
                           const dpf_amd_value_type* vt, const uint8_t* block_index,
                           const int8_t* key_party, const void* key_value_corrections, void* out,
                           void* seeds_out, uint8_t* control_bits_out, void* stream);
+
+// seeds_out[i] = seeds[idx[i]], cb_out[i] = cb[idx[i]] for i < n (idx in
+// [0, num_src): the per-prefix roots of EvaluateUntil's prefix expansion).
+// Device pointers, 16-byte-aligned seeds, stream-ordered.
+int GatherRoots(int64_t n, const int64_t* idx, int64_t num_src, const void* seeds,
+                const uint8_t* cb, void* seeds_out, uint8_t* cb_out, void* stream);
 
 }  // namespace dpf_amd

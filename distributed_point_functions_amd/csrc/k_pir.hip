@@ -86,6 +86,30 @@ __global__ void KGatherRowsSmall(int64_t n, const int64_t* src_offset, int64_t s
   }
 }
 
+// Per-prefix roots of EvaluateUntil's prefix expansion: the partial
+// evaluation of each prefix's tree index (idx, computed on the host and in
+// range by construction; clamped so a corrupted index cannot read outside).
+__global__ void KGatherRoots(int64_t n, const int64_t* idx, int64_t num_src, const uint4* seeds,
+                             const uint8_t* cb, uint4* seeds_out, uint8_t* cb_out) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
+    int64_t j = idx[i];
+    j = j < 0 ? 0 : j >= num_src ? num_src - 1 : j;
+    seeds_out[i] = seeds[j];
+    cb_out[i] = cb[j];
+  }
+}
+
+int GatherRoots(int64_t n, const int64_t* idx, int64_t num_src, const void* seeds,
+                const uint8_t* cb, void* seeds_out, uint8_t* cb_out, void* stream) {
+  if (n <= 0) return DPF_AMD_OK;
+  if (num_src <= 0) return SetError(DPF_AMD_INTERNAL, "no roots to gather from");
+  const int grid = (int)std::min<int64_t>(2048, (n + 255) / 256);
+  hipLaunchKernelGGL(KGatherRoots, dim3(grid), dim3(256), 0, (hipStream_t)stream, n, idx, num_src,
+                     (const uint4*)seeds, cb, (uint4*)seeds_out, cb_out);
+  return LaunchCheck("gather roots kernel launch");
+}
+
 // Host-to-device upload as a kernel on the caller's stream: 16-byte words
 // (the tail byte-wise) read from pinned host memory mapped into the device
 // address space.
@@ -349,39 +373,74 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
 #define DPF_SCAN_M4_READ_BATCH 16  // ds_read_b128 issued back to back
 #endif
 
-// One 128-record tile, its records read through a buffer resource based at
-// the tile (nontemporal).  The record offset goes in voffset, which the
-// range check covers: the last, partial tile limits the range to the bytes
-// left after `base`, so records past num_records read as zero, and lanes
-// past the slice's width use an offset beyond any range.  (One code path for
-// full and partial tiles: two inlined copies made the compiler keep two
-// copies of the accumulators, 163 VGPRs instead of ~100.)
-template <int P>
-__device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint4 s,
-                                           uint32_t (&acc)[64 / P], uint32_t* t, int lane,
-                                           int cpart, bool col_ok, int dw_lo) {
-  constexpr int CPL = 16 / P;
-  constexpr int ROW = 17;
+// Cross-tile record prefetch (DPF_SCAN_M4_XTILE, default on): a wave's
+// register queue of prefetched records runs across its tiles — the last steps
+// of a tile load the first records of the wave's next tile (and the next
+// tile's selection block is loaded at the start of the current one), so a
+// tile starts with its records in flight instead of waiting one HBM latency,
+// and no record is read twice.  (Off: the last steps re-read the tile's own
+// first records, 8 records per 128 = 6 % more HBM reads, r03w_pmc.json:
+// 19.32 GB read for 17.72 GB algorithmic at Q = 64.)
+#ifndef DPF_SCAN_M4_XTILE
+#define DPF_SCAN_M4_XTILE 1
+#endif
+
+// The buffer resource of one 128-record tile, based at the tile.  The record
+// offset goes in voffset, which the range check covers: the last, partial
+// tile limits the range to the bytes left after its base, so records past
+// num_records read as zero, and lanes past the slice's width use an offset
+// beyond any range.  A tile past the end gets an empty range (its loads
+// return zero without touching memory).  (One code path for full and
+// partial tiles: two inlined copies made the compiler keep two copies of the
+// accumulators, 163 VGPRs instead of ~100.)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t M4TileRsrc(const ScanArgs& a, int64_t tile,
+                                                            int dw_lo) {
   const int rec_dwords = a.C * 4;
   const int64_t rec0 = tile << 7;
+  if (rec0 >= a.num_records)
+    return __builtin_amdgcn_make_buffer_rsrc((void*)a.db, 0, 0, 0x00020000);
   const bool full = rec0 + 128 <= a.num_records;
   const uint32_t* base = reinterpret_cast<const uint32_t*>(a.db) + rec0 * rec_dwords + dw_lo;
   const int64_t left = (a.num_records - rec0) * rec_dwords * 4 - dw_lo * 4;
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)base, 0, full ? 0x7fffffff : (int)left, 0x00020000);
-  // record offsets stay below 128 * rec_bytes <= 2^27 (see UseScanM4)
-  const int voff = col_ok ? lane * 4 : (int)0x80000000u;
-  const int rec_bytes = rec_dwords * 4;
-  auto load = [&](int r) -> uint32_t {
-    return __builtin_amdgcn_raw_buffer_load_b32(rsrc, col_ok ? voff + r * rec_bytes : voff, 0, 2);
-  };
-  // records of the next PF groups in flight (a rotating register queue);
-  // the last groups re-read the tile's first, cached, records rather than
-  // branching
-  constexpr int PF = DPF_SCAN_M4_PREFETCH;
-  uint32_t xq[4 * PF];
-#pragma unroll
-  for (int i = 0; i < 4 * PF; ++i) xq[i] = load(i);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, full ? 0x7fffffff : (int)left,
+                                           0x00020000);
+}
+
+// record r (< 128) of the tile behind `rs`, dword `lane` of the slice
+// (record offsets stay below 128 * rec_bytes <= 2^27, see UseScanM4)
+__device__ __forceinline__ uint32_t M4Load(__amdgpu_buffer_rsrc_t rs, int voff, int rec_bytes,
+                                           bool col_ok, int r) {
+  return __builtin_amdgcn_raw_buffer_load_b32(rs, col_ok ? voff + r * rec_bytes : voff, 0, 2);
+}
+
+// Prefetch slot idx of a step: record idx of this tile, or (idx >= 128, the
+// last steps) record idx - 128 of the next tile — or, without XTILE, the
+// current tile's record idx & 127 again.
+__device__ __forceinline__ uint32_t M4Prefetch(__amdgpu_buffer_rsrc_t rs,
+                                               __amdgpu_buffer_rsrc_t rn, int voff,
+                                               int rec_bytes, bool col_ok, int idx) {
+#if DPF_SCAN_M4_XTILE
+  return M4Load(idx >= 128 ? rn : rs, voff, rec_bytes, col_ok, idx & 127);
+#else
+  (void)rn;
+  return M4Load(rs, voff, rec_bytes, col_ok, idx & 127);
+#endif
+}
+
+// One 128-record tile, 4 records per step, one table per wave.  `xq` holds
+// the tile's first 4 * PF records on entry (prefetched) and the next tile's on
+// return.
+constexpr int kM4Prefetch = DPF_SCAN_M4_PREFETCH;
+template <int P>
+__device__ __forceinline__ void ScanM4Tile(uint4 s, __amdgpu_buffer_rsrc_t rs,
+                                           __amdgpu_buffer_rsrc_t rn, int voff, int rec_bytes,
+                                           bool col_ok, uint32_t (&xq)[4 * kM4Prefetch],
+                                           uint32_t (&acc)[64 / P], uint32_t* t, int lane,
+                                           int cpart) {
+  constexpr int CPL = 16 / P;
+  constexpr int ROW = 17;
+  // records of the next PF groups in flight (a rotating register queue)
+  constexpr int PF = kM4Prefetch;
   // step k: records 4k..4k+3, table row e
   auto step = [&](int k, int e) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -393,7 +452,8 @@ __device__ __forceinline__ void ScanM4Tile(const ScanArgs& a, int64_t tile, uint
 #pragma unroll
     for (int i = 0; i < 4 * (PF - 1); ++i) xq[i] = xq[i + 4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xq[4 * (PF - 1) + i] = load((4 * (k + PF) + i) & 127);
+    for (int i = 0; i < 4; ++i)
+      xq[4 * (PF - 1) + i] = M4Prefetch(rs, rn, voff, rec_bytes, col_ok, 4 * (k + PF) + i);
     const uint32_t x01 = x[0] ^ x[1], x012 = x01 ^ x[2];
     const uint32_t r[16] = {0u,          x[0],        x[1],        x01,
                             x[2],        x[0] ^ x[2], x[1] ^ x[2], x012,
@@ -519,30 +579,17 @@ __device__ __forceinline__ uint32_t Xor3(uint32_t a, uint32_t b, uint32_t c) {
         : "memory");                                                                      \
   } while (0)
 
+// the next DPF steps' records (8 each) in flight at P = 2
+constexpr int M4DualPrefetch(int P) { return P == 2 ? DPF_SCAN_M4_DUAL_PF : 1; }
+
 template <int P>
-__device__ __forceinline__ void ScanM4Tile2(const ScanArgs& a, int64_t tile, uint4 s,
-                                            uint32_t (&acc)[64 / P], uint32_t* t, int lane,
-                                            int cpart, bool col_ok, int dw_lo) {
+__device__ __forceinline__ void ScanM4Tile2(uint4 s, __amdgpu_buffer_rsrc_t rs,
+                                            __amdgpu_buffer_rsrc_t rn, int voff, int rec_bytes,
+                                            bool col_ok, uint32_t (&xq)[8 * M4DualPrefetch(P)],
+                                            uint32_t (&acc)[64 / P], uint32_t* t, int cpart) {
   constexpr int CPL = 16 / P;
   constexpr int ROW = 17;
-  const int rec_dwords = a.C * 4;
-  const int64_t rec0 = tile << 7;
-  const bool full = rec0 + 128 <= a.num_records;
-  const uint32_t* base = reinterpret_cast<const uint32_t*>(a.db) + rec0 * rec_dwords + dw_lo;
-  const int64_t left = (a.num_records - rec0) * rec_dwords * 4 - dw_lo * 4;
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)base, 0, full ? 0x7fffffff : (int)left, 0x00020000);
-  const int voff = col_ok ? lane * 4 : (int)0x80000000u;
-  const int rec_bytes = rec_dwords * 4;
-  auto load = [&](int r) -> uint32_t {
-    return __builtin_amdgcn_raw_buffer_load_b32(rsrc, col_ok ? voff + r * rec_bytes : voff, 0, 2);
-  };
-  // the next DPF steps' records (8 each) in flight; the last steps re-read
-  // the tile's first (cached) records rather than branching
-  constexpr int DPF = P == 2 ? DPF_SCAN_M4_DUAL_PF : 1;
-  uint32_t xq[8 * DPF];
-#pragma unroll
-  for (int i = 0; i < 8 * DPF; ++i) xq[i] = load(i);
+  constexpr int DPF = M4DualPrefetch(P);
   // step k: records 8k..8k+7 into tables A and B, selection byte sb
   auto step = [&](int k, uint32_t sb) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -557,7 +604,8 @@ __device__ __forceinline__ void ScanM4Tile2(const ScanArgs& a, int64_t tile, uin
 #pragma unroll
     for (int i = 0; i < 8 * (DPF - 1); ++i) xq[i] = xq[i + 8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) xq[8 * (DPF - 1) + i] = load((8 * (k + DPF) + i) & 127);
+    for (int i = 0; i < 8; ++i)
+      xq[8 * (DPF - 1) + i] = M4Prefetch(rs, rn, voff, rec_bytes, col_ok, 8 * (k + DPF) + i);
     DPF_M4_STORE_TABLE(0, xa);
     DPF_M4_STORE_TABLE(4352, xb);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -632,13 +680,33 @@ void KPirScanM4(ScanArgs a) {
 #pragma unroll
   for (int i = 0; i < 4 * CPL; ++i) acc[i] = 0u;
   const int64_t tiles = (a.num_records + 127) >> 7;
-  for (int64_t tile = part; tile < tiles; tile += a.parts) {
-    const uint4 s = q_ok ? a.sel[(int64_t)(a.q0 + q) * a.sel_blocks + tile]
-                         : make_uint4(0, 0, 0, 0);
-    if (DUAL)
-      ScanM4Tile2<P>(a, tile, s, acc, t, lane, cpart, col_ok, dw_lo);
-    else
-      ScanM4Tile<P>(a, tile, s, acc, t, lane, cpart, col_ok, dw_lo);
+  const int rec_bytes = a.C * 16;
+  const int voff = col_ok ? lane * 4 : (int)0x80000000u;
+  constexpr int XQ = DUAL ? 8 * M4DualPrefetch(P) : 4 * kM4Prefetch;
+  int64_t tile = part;
+  if (tile < tiles) {  // wave-uniform
+    __amdgpu_buffer_rsrc_t rs = M4TileRsrc(a, tile, dw_lo);
+    uint4 s = q_ok ? a.sel[(int64_t)(a.q0 + q) * a.sel_blocks + tile] : make_uint4(0, 0, 0, 0);
+    uint32_t xq[XQ];
+#pragma unroll
+    for (int i = 0; i < XQ; ++i) xq[i] = M4Load(rs, voff, rec_bytes, col_ok, i);
+    for (;;) {
+      const int64_t next = tile + a.parts;
+      const bool more = next < tiles;
+      // the next tile's resource (an empty range past the end) and selection
+      // block, in flight while this tile runs
+      const __amdgpu_buffer_rsrc_t rn = M4TileRsrc(a, next, dw_lo);
+      const uint4 sn = (q_ok && more) ? a.sel[(int64_t)(a.q0 + q) * a.sel_blocks + next]
+                                      : make_uint4(0, 0, 0, 0);
+      if constexpr (DUAL)
+        ScanM4Tile2<P>(s, rs, rn, voff, rec_bytes, col_ok, xq, acc, t, cpart);
+      else
+        ScanM4Tile<P>(s, rs, rn, voff, rec_bytes, col_ok, xq, acc, t, lane, cpart);
+      if (!more) break;
+      tile = next;
+      rs = rn;
+      s = sn;
+    }
   }
   if (!q_ok) return;
   // this lane's columns [cpart * CPL, +CPL) of the slice, clipped to the record
@@ -720,36 +788,36 @@ void KPirScanM4Pair(ScanArgs a) {
 #pragma unroll
   for (int i = 0; i < 64; ++i) acc[i] = 0u;
   const int64_t tiles = (a.num_records + 127) >> 7;
-  const int rec_dwords = a.C * 4;
-  const int rec_bytes = rec_dwords * 4;
-  for (int64_t tile = part; tile < tiles; tile += a.parts) {
-    const uint4 s = q_ok ? a.sel[(int64_t)(a.q0 + q) * a.sel_blocks + tile]
-                         : make_uint4(0, 0, 0, 0);
-    const int64_t rec0 = tile << 7;
-    const bool full = rec0 + 128 <= a.num_records;
-    const uint32_t* base =
-        reinterpret_cast<const uint32_t*>(a.db) + rec0 * rec_dwords + dw_lo;
-    const int64_t left = (a.num_records - rec0) * rec_dwords * 4 - dw_lo * 4;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)base, 0, full ? 0x7fffffff : (int)left, 0x00020000);
-    const int voff = col_ok ? lane * 4 : (int)0x80000000u;
-    auto load = [&](int r) -> uint32_t {
-      return __builtin_amdgcn_raw_buffer_load_b32(rsrc, col_ok ? voff + r * rec_bytes : voff, 0,
-                                                  2);
-    };
-    // this wave's 4 records of the next step in flight
+  const int rec_bytes = a.C * 16;
+  const int voff = col_ok ? lane * 4 : (int)0x80000000u;
+  int64_t tile = part;
+  if (tile < tiles) {  // block-uniform
+    __amdgpu_buffer_rsrc_t rs = M4TileRsrc(a, tile, dw_lo);
+    uint4 s = q_ok ? a.sel[(int64_t)(a.q0 + q) * a.sel_blocks + tile] : make_uint4(0, 0, 0, 0);
+    // this wave's 4 records of the next step in flight (across tiles)
     uint32_t xq[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xq[i] = load(4 * wave + i);
+    for (int i = 0; i < 4; ++i) xq[i] = M4Load(rs, voff, rec_bytes, col_ok, 4 * wave + i);
+    for (;;) {
+      const int64_t next = tile + a.parts;
+      const bool more = next < tiles;
+      const __amdgpu_buffer_rsrc_t rn = M4TileRsrc(a, next, dw_lo);
+      const uint4 sn = (q_ok && more) ? a.sel[(int64_t)(a.q0 + q) * a.sel_blocks + next]
+                                      : make_uint4(0, 0, 0, 0);
 #pragma unroll 1
-    for (int k = 0; k < 16; ++k) {
-      uint32_t x[4];
+      for (int k = 0; k < 16; ++k) {
+        uint32_t x[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        x[i] = xq[i];
-        xq[i] = load((8 * (k + 1) + 4 * wave + i) & 127);
+        for (int i = 0; i < 4; ++i) {
+          x[i] = xq[i];
+          xq[i] = M4Prefetch(rs, rn, voff, rec_bytes, col_ok, 8 * (k + 1) + 4 * wave + i);
+        }
+        ScanM4PairStep(x, (SelWord(s, k >> 2) >> (8 * (k & 3))) & 255, k & 1, t, tab0, acc);
       }
-      ScanM4PairStep(x, (SelWord(s, k >> 2) >> (8 * (k & 3))) & 255, k & 1, t, tab0, acc);
+      if (!more) break;
+      tile = next;
+      rs = rn;
+      s = sn;
     }
   }
   if (!q_ok) return;

@@ -261,15 +261,26 @@ __global__ __launch_bounds__(kPointsBlockOf<BN>, kPointsWavesOf<BN>) void KEvalu
 // the left/right difference and the value key in registers (33 VGPRs).
 // Semantics are those of PointsIter (walk, value hash, emit) for BN <= 2.
 
-template <int BN>
+// T4: four 64 KiB-halved tables (aes_device.h FillTables4, 128 KiB per
+// block), for launches of at most kQuadT4MaxPoints points (one block per CU).
+template <int BN, bool T4>
 __global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluatePointsQuad(PointsArgs a,
                                                                                    VtDev vt) {
-  __shared__ uint32_t tab[kTabWords];
-  FillTables(tab);
+  __shared__ uint32_t tab[T4 ? kTab4Words : kTabWords];
+  if constexpr (T4)
+    FillTables4(tab);
+  else
+    FillTables(tab);
   __syncthreads();
-  const Lds L = MakeLds(tab);
+  using LT = std::conditional_t<T4, Lds4, Lds>;
+  LT L;
+  if constexpr (T4)
+    L = MakeLds4(tab);
+  else
+    L = MakeLds(tab);
   const int c = threadIdx.x & 3;
   const QuadKey kl = MakeQuadKey<0>(c), kv = MakeQuadKey<2>(c);
+  const QuadRk klr = MakeQuadRk<0>(c), kvr = MakeQuadRk<2>(c);
   const QuadDiff kd = MakeQuadDiff(c);
   const WalkArgs& w = a.w;
   const int64_t ppk = w.points_per_key;
@@ -296,7 +307,10 @@ __global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluatePointsQua
     for (int level = 0; level < w.num_levels; ++level) {
       const uint32_t bit = PathBit(p, w.num_levels - level - 1 + w.rightshift);
       const int64_t ci = cw_base + level * cw_step;
-      QuadWalkStep(x, t, bit, cw_words[ci * 4 + c], w.ccl[ci], w.ccr[ci], c, kl, kd, L);
+      if constexpr (T4 || DPF_QUAD_RKM)
+        QuadWalkStepRk<T4>(x, t, bit, cw_words[ci * 4 + c], w.ccl[ci], w.ccr[ci], c, klr, kd, L);
+      else
+        QuadWalkStep(x, t, bit, cw_words[ci * 4 + c], w.ccl[ci], w.ccr[ci], c, kl, kd, L);
     }
     if (w.seeds_out) {
       reinterpret_cast<uint32_t*>(w.seeds_out)[i * 4 + c] = x;
@@ -317,7 +331,11 @@ __global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluatePointsQua
         in = (uint32_t)(v >> (32 * c));
       }
       const uint32_t sg = SigmaQuad(in, c);
-      const uint32_t h = AesQuad<false>(sg, kv, kd, 0u, L) ^ sg;
+      uint32_t h;
+      if constexpr (T4 || DPF_QUAD_RKM)
+        h = AesQuadRk<T4>(sg, kvr, L) ^ sg;
+      else
+        h = AesQuad<false>(sg, kv, kd, 0u, L) ^ sg;
       const uint32_t h0 = QuadPerm<kQuadBcast<0>>(h), h1 = QuadPerm<kQuadBcast<1>>(h),
                      h2 = QuadPerm<kQuadBcast<2>>(h), h3 = QuadPerm<kQuadBcast<3>>(h);
       W[j] = (u128)h0 | ((u128)h1 << 32) | ((u128)h2 << 64) | ((u128)h3 << 96);
@@ -631,11 +649,24 @@ static void LaunchPoints(int64_t n, hipStream_t st, const PointsArgs& a, const V
   hipLaunchKernelGGL((KEvaluatePoints<BN>), dim3(grid), dim3(block), 0, st, a, vt);
 }
 
+// Four-table quad walk up to this many points: one 128 KiB-table block per
+// CU holds the launch (<= 512 lanes per CU) in one resident round.
+#ifndef DPF_QUAD_T4_MAX
+#define DPF_QUAD_T4_MAX (256 * kPointsBlock / 4)
+#endif
 template <int BN>
 static void LaunchPointsQuad(int64_t n, hipStream_t st, const PointsArgs& a, const VtDev& vt) {
+  if (n <= DPF_QUAD_T4_MAX) {
+    // one block per CU: 4n lanes over 256 blocks
+    const int64_t per = ((4 * n + 255) / 256 + 63) / 64 * 64;
+    const int block = (int)std::min<int64_t>(kPointsBlock, std::max<int64_t>(64, per));
+    const int grid = (int)std::min<int64_t>(DPF_WALK_MAX_GRID, (4 * n + block - 1) / block);
+    hipLaunchKernelGGL((KEvaluatePointsQuad<BN, true>), dim3(grid), dim3(block), 0, st, a, vt);
+    return;
+  }
   const int block = WalkBlock(4 * n, kPointsBlock);
   const int grid = (int)std::min<int64_t>(DPF_WALK_MAX_GRID, (4 * n + block - 1) / block);
-  hipLaunchKernelGGL((KEvaluatePointsQuad<BN>), dim3(grid), dim3(block), 0, st, a, vt);
+  hipLaunchKernelGGL((KEvaluatePointsQuad<BN, false>), dim3(grid), dim3(block), 0, st, a, vt);
 }
 
 // Points below which the quad-lane walk runs (one-chain lanes fill the chip

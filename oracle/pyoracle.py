@@ -140,6 +140,8 @@ def _ptr(a: np.ndarray):
 
 # ---------------------------------------------------------------- helpers
 def u128_words(values: Sequence[int]) -> np.ndarray:
+    if isinstance(values, np.ndarray):  # (n, 2) {lo, hi} words already
+        return np.ascontiguousarray(values, dtype=np.uint64).reshape(-1)
     out = np.empty(2 * len(values), dtype=np.uint64)
     for i, v in enumerate(values):
         v = int(v)

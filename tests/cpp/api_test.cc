@@ -111,6 +111,42 @@ static int IncrementalTuple() {
   return 0;
 }
 
+// distributed_point_function_test.cc:190-235 (TestSinglePointPartialEvaluation):
+// EvaluateAt<uint32_t>(0, {prefix}, ctx) at a 108-bit level, then
+// EvaluateUntil<uint32_t>(1, {prefix}, ctx) from the stored evaluation.
+static int SinglePointPartialEvaluation() {
+  std::vector<DpfParameters> ps(2);
+  ps[0].set_log_domain_size(108);
+  ps[1].set_log_domain_size(128);
+  for (auto& p : ps) p.mutable_value_type()->mutable_integer()->set_bitsize(32);
+  auto dpf = DistributedPointFunction::CreateIncremental(ps);
+  CHECK_OK(dpf);
+  const uint128 prefix = 0xdeadbeef, suffix = 23;
+  const uint128 alpha = (prefix << 20) + suffix;
+  const uint32_t beta = 42;
+  auto keys = (*dpf)->GenerateKeysIncremental(alpha, std::vector<uint128>{beta, beta});
+  CHECK_OK(keys);
+  auto ca = (*dpf)->CreateEvaluationContext(keys->first);
+  auto cb = (*dpf)->CreateEvaluationContext(keys->second);
+  CHECK_OK(ca);
+  CHECK_OK(cb);
+  std::vector<uint128> pre = {prefix};
+  auto ra = (*dpf)->EvaluateAt<uint32_t>(0, pre, *ca);
+  auto rb = (*dpf)->EvaluateAt<uint32_t>(0, pre, *cb);
+  CHECK_OK(ra);
+  CHECK_OK(rb);
+  CHECK(uint32_t((*ra)[0] + (*rb)[0]) == beta);
+  CHECK(ca->previous_hierarchy_level() == 0 && ca->partial_evaluations_size() == 1);
+  auto ua = (*dpf)->EvaluateUntil<uint32_t>(1, pre, *ca);
+  auto ub = (*dpf)->EvaluateUntil<uint32_t>(1, pre, *cb);
+  CHECK_OK(ua);
+  CHECK_OK(ub);
+  CHECK(ua->size() == (size_t{1} << 20) && ub->size() == ua->size());
+  for (size_t i = 0; i < ua->size(); ++i)
+    CHECK(uint32_t((*ua)[i] + (*ub)[i]) == (i == suffix ? beta : 0u));
+  return 0;
+}
+
 static int DcfGenEval() {
   DcfParameters p;
   p.mutable_parameters()->set_log_domain_size(5);
@@ -375,7 +411,8 @@ static int PirShardedPlainRequests() {
 }
 
 int main() {
-  if (FullDomainUint64() || IncrementalTuple() || DcfGenEval() || Registration() ||
+  if (FullDomainUint64() || IncrementalTuple() || SinglePointPartialEvaluation() ||
+      DcfGenEval() || Registration() ||
       EvaluateAndApplyStops() || IncrementalManyPrefixes() || EvaluateAndApplyRepeatedKeys() ||
       PirShardedPlainRequests())
     return 2;

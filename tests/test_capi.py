@@ -99,3 +99,27 @@ def test_walk_and_dcf_kernel_hooks_validate_and_are_per_thread():
     assert seen == {"walk": 0, "dcf": 0}
     assert L.dpf_amd_set_walk_mode(0) == 1
     assert L.dpf_amd_set_dcf_kernel(0) == 1
+
+
+def test_prefix_expand_and_thread_cache_hooks():
+    """dpf_amd_set_prefix_expand (0 / 1) is per thread and refuses other
+    values; dpf_amd_set_thread_cache_cap refuses a negative cap (no GPU: the
+    setters touch no device state)."""
+    import threading
+    from distributed_point_functions_amd import _lib
+    L = _lib.lib()
+    assert L.dpf_amd_set_prefix_expand(2) == -2
+    assert L.dpf_amd_set_prefix_expand(1) == 0
+    seen = {}
+
+    def other():
+        seen["mode"] = L.dpf_amd_set_prefix_expand(0)
+
+    t = threading.Thread(target=other)
+    t.start()
+    t.join()
+    assert seen == {"mode": 0}
+    assert L.dpf_amd_set_prefix_expand(0) == 1
+    assert L.dpf_amd_set_thread_cache_cap(-1) == 3
+    assert b"cap" in L.dpf_amd_last_error()
+    assert L.dpf_amd_set_thread_cache_cap(64) == 0

@@ -69,10 +69,24 @@ def _evaluator(dpf, od, hier, ctxs, octxs):
     return evaluate
 
 
+@pytest.fixture(params=[0, 1], ids=["prefix_expand", "unique_expand_gather"])
+def expand_mode(request, api):
+    """EvaluateUntil's two strategies for calls with prefixes
+    (dpf_amd_set_prefix_expand): each prefix's subtree expanded straight into
+    the output, or the unique tree indices expanded and gathered."""
+    from distributed_point_functions_amd import _lib
+    L = _lib.lib()
+    prev = L.dpf_amd_set_prefix_expand(request.param)
+    yield request.param
+    L.dpf_amd_set_prefix_expand(prev)
+
+
 @pytest.mark.parametrize("single_point", [False, True])
 @pytest.mark.parametrize("suite", IC.SUITES, ids=[s[0] for s in IC.SUITES])
-def test_incremental_dpf_correctness_vs_oracle(api, suite, single_point):
+def test_incremental_dpf_correctness_vs_oracle(api, suite, single_point, expand_mode):
     name, hier, alphas, betas_list, steps = suite
+    if single_point and expand_mode:
+        pytest.skip("EvaluateAt does not expand")
     levels = IC.levels_of(hier)
     dpf = _make(api, levels)
     od = po.Dpf(levels)
@@ -88,7 +102,7 @@ def test_incremental_dpf_correctness_vs_oracle(api, suite, single_point):
                             _evaluator(dpf, od, hier, ctxs, octxs))
 
 
-def test_single_point_partial_evaluation_then_evaluate_until(api):
+def test_single_point_partial_evaluation_then_evaluate_until(api, expand_mode):
     """test.cc:190-235: EvaluateAt(0, {prefix}, ctx) at a 108-bit level, then
     EvaluateUntil(1, {prefix}, ctx) expands the 2^20 suffixes below it from
     the stored partial evaluation — every output and context vs the oracle."""
@@ -116,7 +130,7 @@ def test_single_point_partial_evaluation_then_evaluate_until(api):
     assert np.array_equal(s, want)
 
 
-def test_mixed_evaluate_until_and_evaluate_at_ctx(api):
+def test_mixed_evaluate_until_and_evaluate_at_ctx(api, expand_mode):
     """EvaluateUntil on level 0 and 1 (partial evaluations stored at level
     0), then EvaluateAt with the context two levels further down (a walk of
     the stored evaluations over several tree levels), then a level-skipping
