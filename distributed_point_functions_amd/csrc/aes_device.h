@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "aes_tables.h"
 #include "dpf_amd.h"
@@ -26,6 +27,12 @@
 #endif
 #ifndef DPF_VALUE_PAIRS
 #define DPF_VALUE_PAIRS 1  // AesPairs for the value PRG of even seeds
+#endif
+#ifndef DPF_BS_LAST
+#define DPF_BS_LAST 0  // experiment: the tree pair's last AES round on the VALU
+#endif
+#if DPF_BS_LAST
+#include "bs_last_round.h"
 #endif
 #ifndef DPF_LANE_WALK
 #define DPF_LANE_WALK 1  // divergent walk levels: 1 AES with a per-lane key
@@ -87,6 +94,7 @@ constexpr AesKey kDpfKeys[3] = {ExpandAesKey(kPrgKeyLeftLo, kPrgKeyLeftHi),
 // post(n, i, w) is applied after round-key word i entered state n's word
 // (identity except for per-lane masked keys).
 struct KeyNoPost {
+  static constexpr bool kBsLast = false;  // keys the VALU last round may use
   __device__ __forceinline__ uint32_t post(int, int, uint32_t w) const { return w; }
 };
 template <int W>
@@ -94,7 +102,14 @@ struct DpfKeyAt : KeyNoPost {  // one fixed DPF key for all states
   __device__ __forceinline__ uint32_t rk(int, int i) const { return kDpfKeys[W].rk[i]; }
   __device__ __forceinline__ uint32_t rkr(int, int i) const { return kDpfKeys[W].rkr[i]; }
 };
+// Key classes that declare kBsLast = true (the tree pair's fixed keys).
+template <class K, class = void>
+struct BsLastKey : std::false_type {};
+template <class K>
+struct BsLastKey<K, std::enable_if_t<K::kBsLast>> : std::true_type {};
+
 struct DpfLeftRight : KeyNoPost {  // state 0: left key, state 1: right key
+  static constexpr bool kBsLast = true;
   __device__ __forceinline__ uint32_t rk(int n, int i) const { return kDpfKeys[n].rk[i]; }
   __device__ __forceinline__ uint32_t rkr(int n, int i) const { return kDpfKeys[n].rkr[i]; }
 };
@@ -184,6 +199,25 @@ __device__ __forceinline__ void AesFromRound(uint32_t (&w)[N][4], const K& key,
 #pragma unroll
     for (int n = 0; n < N; ++n) RoundCombine(t[n], key, n, r, w[n]);
   }
+#if DPF_BS_LAST
+  // (experiment) the tree pair's last round on the VALU:
+  // bitsliced SubBytes over both states, then ShiftRows + the round key as
+  // two v_perm + one XOR3 per column — no LDS lookups.
+  if constexpr (N == 2 && BsLastKey<K>::value) {
+    uint32_t R[8] = {w[0][0], w[0][1], w[0][2], w[0][3], w[1][0], w[1][1], w[1][2], w[1][3]};
+    BsSubBytes8(R);
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t lo = __builtin_amdgcn_perm(R[4 * n + ((c + 1) & 3)], R[4 * n + c], 0x0c0c0500u);
+        const uint32_t hi =
+            __builtin_amdgcn_perm(R[4 * n + ((c + 3) & 3)], R[4 * n + ((c + 2) & 3)], 0x07020c0cu);
+        w[n][c] = key.post(n, 40 + c, Xor3(lo, hi, key.rk(n, 40 + c)));
+      }
+    return;
+  }
+#endif
   // Last round: S-box bytes are byte 1/2 of T0 and byte 3 of T1.
   uint32_t t[N][4][4];
 #pragma unroll

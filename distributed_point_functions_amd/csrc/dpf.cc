@@ -1077,6 +1077,8 @@ struct IncrementalScratch {
   uint128* seeds = nullptr;  // pinned
   uint8_t* cbs = nullptr;    // pinned
   int* flag = nullptr;       // pinned: the gather's error flag (an async copy)
+  int32_t* pidx = nullptr;   // pinned: per-prefix unique-root index (prefix expansion)
+  uint8_t* plow = nullptr;   // pinned: per-prefix bits below its tree index
   size_t cap = 0;
   hipEvent_t done = nullptr;
   int device = -1;
@@ -1089,6 +1091,8 @@ struct IncrementalScratch {
     if (seeds) (void)hipHostFree(seeds);
     if (cbs) (void)hipHostFree(cbs);
     if (flag) (void)hipHostFree(flag);
+    if (pidx) (void)hipHostFree(pidx);
+    if (plow) (void)hipHostFree(plow);
   }
   Status Reserve(size_t n) {
     if (!flag) DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc((void**)&flag, 64, 0), "hipHostMalloc"));
@@ -1108,15 +1112,21 @@ struct IncrementalScratch {
     if (tree) (void)hipHostFree(tree);
     if (seeds) (void)hipHostFree(seeds);
     if (cbs) (void)hipHostFree(cbs);
+    if (pidx) (void)hipHostFree(pidx);
+    if (plow) (void)hipHostFree(plow);
     tree = nullptr;
     seeds = nullptr;
     cbs = nullptr;
+    pidx = nullptr;
+    plow = nullptr;
     cap = 0;
     size_t c = 1024;
     while (c < n) c <<= 1;
     DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc((void**)&tree, 16 * c, 0), "hipHostMalloc"));
     DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc((void**)&seeds, 16 * c, 0), "hipHostMalloc"));
     DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc((void**)&cbs, c, 0), "hipHostMalloc"));
+    DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc((void**)&pidx, 4 * c, 0), "hipHostMalloc"));
+    DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc((void**)&plow, c, 0), "hipHostMalloc"));
     cap = c;
     return OkStatus();
   }
@@ -1432,11 +1442,11 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   // no gather runs (c3: 2^16 prefixes, half the AES and none of the 256 MiB
   // staging round trip).  `src` then holds each prefix's unique-root index.
   const bool fused = !dpf_amd::PrefixExpandOff() && !prefixes.empty() &&
-                     stop_level >= previous_log_domain_size;
+                     stop_level >= previous_log_domain_size && num_prefixes < (int64_t{1} << 31);
   if (!prefixes.empty()) {
     const int bbits = st.parameters[prev_h].log_domain_size() - st.hierarchy_to_tree[prev_h];
     const uint64_t bmask = (uint64_t{1} << bbits) - 1;  // bbits <= 7 (epb <= 128)
-    if (static_cast<int64_t>(src.size()) < num_prefixes) src.resize(num_prefixes);
+    if (!fused && static_cast<int64_t>(src.size()) < num_prefixes) src.resize(num_prefixes);
     constexpr int kParts = static_cast<int>(HostPool::kWorkers) + 1;
     int64_t count[kParts] = {}, first[kParts] = {};
     bool ordered[kParts];
@@ -1467,10 +1477,14 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
         for (int64_t i = b; i < e; ++i) {
           const uint128 t = prefixes[i] >> bbits;
           if (i == 0 || t != (prefixes[i - 1] >> bbits)) tree_indices[u++] = t;
-          src[i] = fused ? u - 1
-                         : (u - 1) * seg +
-                               static_cast<int64_t>(static_cast<uint64_t>(prefixes[i]) & bmask) *
-                                   outputs_per_prefix;
+          if (fused) {
+            sc.pidx[i] = static_cast<int32_t>(u - 1);
+            sc.plow[i] = static_cast<uint8_t>(static_cast<uint64_t>(prefixes[i]) & bmask);
+          } else {
+            src[i] = (u - 1) * seg +
+                     static_cast<int64_t>(static_cast<uint64_t>(prefixes[i]) & bmask) *
+                         outputs_per_prefix;
+          }
         }
       });
     } else {
@@ -1481,10 +1495,14 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
         const uint128 ti = prefixes[i] >> bbits;
         auto it = inverse.emplace(ti, num_unique);
         if (it.second) tree_indices[num_unique++] = ti;
-        src[i] = fused ? it.first->second
-                       : it.first->second * seg +
-                             static_cast<int64_t>(static_cast<uint64_t>(prefixes[i]) & bmask) *
-                                 outputs_per_prefix;
+        if (fused) {
+          sc.pidx[i] = static_cast<int32_t>(it.first->second);
+          sc.plow[i] = static_cast<uint8_t>(static_cast<uint64_t>(prefixes[i]) & bmask);
+        } else {
+          src[i] = it.first->second * seg +
+                   static_cast<int64_t>(static_cast<uint64_t>(prefixes[i]) & bmask) *
+                       outputs_per_prefix;
+        }
       }
     }
   }
@@ -1520,35 +1538,37 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
     CwArrays wc = KeyCws(ctx.key(), prev_tree, previous_log_domain_size);
     CwArrays ec = KeyCws(ctx.key(), previous_log_domain_size, stop_level);
     using Part = UploadRing::HostPart;
-    // every input in one packed upload: root index per prefix, the prefixes
-    // (the walk's paths), both correction-word ranges
-    const Part parts[8] = {{src.data(), size_t(8) * num_prefixes},
-                           {prefixes.data(), walk ? size_t(16) * num_prefixes : 0},
-                           {wc.seeds.data(), size_t(16) * walk},
+    // both correction-word ranges through the upload ring; the per-prefix
+    // root index and low bits DMA'd straight from the pinned scratch
+    const Part parts[6] = {{wc.seeds.data(), size_t(16) * walk},
                            {wc.ccl.data(), size_t(walk)},
                            {wc.ccr.data(), size_t(walk)},
                            {ec.seeds.data(), size_t(16) * down},
                            {ec.ccl.data(), size_t(down)},
                            {ec.ccr.data(), size_t(down)}};
-    size_t off[8];
-    const size_t in_bytes = UploadRing::PackedLayout(parts, 8, off);
-    const size_t seeds_off = in_bytes;
+    size_t off[6];
+    const size_t cw_bytes = UploadRing::PackedLayout(parts, 6, off);
+    const size_t idx_off = cw_bytes;
+    const size_t low_off = idx_off + ((size_t(4) * num_prefixes + 15) & ~size_t{15});
+    const size_t seeds_off = low_off + ((size_t(num_prefixes) + 15) & ~size_t{15});
     const size_t cb_off = seeds_off + size_t(16) * num_prefixes;
     DeviceBuffer work, result;
     DPF_RETURN_IF_ERROR(work.Alloc(cb_off + num_prefixes, s));
     char* d = work.as<char>();
-    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 8, in_bytes, off, s));
+    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 6, cw_bytes, off, s));
+    DPF_RETURN_IF_ERROR(HipStatus(hipMemcpyAsync(d + idx_off, sc.pidx, size_t(4) * num_prefixes,
+                                                 hipMemcpyHostToDevice, s),
+                                  "upload"));
+    DPF_RETURN_IF_ERROR(HipStatus(
+        hipMemcpyAsync(d + low_off, sc.plow, size_t(num_prefixes), hipMemcpyHostToDevice, s),
+        "upload"));
     void* pseeds = d + seeds_off;
     uint8_t* pcb = reinterpret_cast<uint8_t*>(d + cb_off);
-    DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd::GatherRoots(
-        num_prefixes, reinterpret_cast<const int64_t*>(d + off[0]), num_unique, root_seeds, root_cb,
-        pseeds, pcb, s)));
-    if (walk > 0)
-      DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_seeds(
-          num_prefixes, walk, walk, pseeds, pcb, d + off[1], 0, d + off[2],
-          reinterpret_cast<const uint8_t*>(d + off[3]), reinterpret_cast<const uint8_t*>(d + off[4]),
-          dpf_amd::kPrgKeyLeftLo, dpf_amd::kPrgKeyLeftHi, dpf_amd::kPrgKeyRightLo,
-          dpf_amd::kPrgKeyRightHi, pseeds, pcb, s)));
+    DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd::PrefixRoots(
+        num_prefixes, reinterpret_cast<const int32_t*>(d + idx_off),
+        reinterpret_cast<const uint8_t*>(d + low_off), walk, num_unique, root_seeds, root_cb,
+        d + off[0], reinterpret_cast<const uint8_t*>(d + off[1]),
+        reinterpret_cast<const uint8_t*>(d + off[2]), pseeds, pcb, s)));
     void* final_dev = out;
     if (!out_on_device) {
       DPF_RETURN_IF_ERROR(result.Alloc(total * stride, s));
@@ -1556,8 +1576,8 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
     }
     DPF_RETURN_IF_ERROR(ClearPadding(vt, final_dev, total * stride, s));
     DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_expand_and_correct(
-        num_prefixes, pseeds, pcb, down, d + off[5], reinterpret_cast<const uint8_t*>(d + off[6]),
-        reinterpret_cast<const uint8_t*>(d + off[7]), &vt,
+        num_prefixes, pseeds, pcb, down, d + off[3], reinterpret_cast<const uint8_t*>(d + off[4]),
+        reinterpret_cast<const uint8_t*>(d + off[5]), &vt,
         reinterpret_cast<const uint64_t*>(corr.data()), ctx.key().party(), cepb, 0,
         num_prefixes << down, final_dev, s)));
     trace.Mark("prefix_expand_launch");

@@ -100,10 +100,12 @@ int EvaluatePointsIndexed(int64_t num_points, const int32_t* key_index, int64_t 
                           const int8_t* key_party, const void* key_value_corrections, void* out,
                           void* seeds_out, uint8_t* control_bits_out, void* stream);
 
-// seeds_out[i] = seeds[idx[i]], cb_out[i] = cb[idx[i]] for i < n (idx in
-// [0, num_src): the per-prefix roots of EvaluateUntil's prefix expansion).
-// Device pointers, 16-byte-aligned seeds, stream-ordered.
-int GatherRoots(int64_t n, const int64_t* idx, int64_t num_src, const void* seeds,
-                const uint8_t* cb, void* seeds_out, uint8_t* cb_out, void* stream);
+// EvaluateUntil's per-prefix roots in one launch: prefix i starts from row
+// idx[i] of seeds / cb (the context walk's output) and walks `walk` (< 8)
+// levels along the bits of low[i] with the DPF keys and correction words
+// [level] (cw_seed / ccl / ccr).  Device pointers, stream-ordered.
+int PrefixRoots(int64_t n, const int32_t* idx, const uint8_t* low, int walk, int64_t num_src,
+                const void* seeds, const uint8_t* cb, const void* cw_seed, const uint8_t* ccl,
+                const uint8_t* ccr, void* seeds_out, uint8_t* cb_out, void* stream);
 
 }  // namespace dpf_amd

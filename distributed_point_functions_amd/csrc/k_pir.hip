@@ -86,30 +86,6 @@ __global__ void KGatherRowsSmall(int64_t n, const int64_t* src_offset, int64_t s
   }
 }
 
-// Per-prefix roots of EvaluateUntil's prefix expansion: the partial
-// evaluation of each prefix's tree index (idx, computed on the host and in
-// range by construction; clamped so a corrupted index cannot read outside).
-__global__ void KGatherRoots(int64_t n, const int64_t* idx, int64_t num_src, const uint4* seeds,
-                             const uint8_t* cb, uint4* seeds_out, uint8_t* cb_out) {
-  const int64_t step = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
-    int64_t j = idx[i];
-    j = j < 0 ? 0 : j >= num_src ? num_src - 1 : j;
-    seeds_out[i] = seeds[j];
-    cb_out[i] = cb[j];
-  }
-}
-
-int GatherRoots(int64_t n, const int64_t* idx, int64_t num_src, const void* seeds,
-                const uint8_t* cb, void* seeds_out, uint8_t* cb_out, void* stream) {
-  if (n <= 0) return DPF_AMD_OK;
-  if (num_src <= 0) return SetError(DPF_AMD_INTERNAL, "no roots to gather from");
-  const int grid = (int)std::min<int64_t>(2048, (n + 255) / 256);
-  hipLaunchKernelGGL(KGatherRoots, dim3(grid), dim3(256), 0, (hipStream_t)stream, n, idx, num_src,
-                     (const uint4*)seeds, cb, (uint4*)seeds_out, cb_out);
-  return LaunchCheck("gather roots kernel launch");
-}
-
 // Host-to-device upload as a kernel on the caller's stream: 16-byte words
 // (the tail byte-wise) read from pinned host memory mapped into the device
 // address space.

@@ -635,6 +635,55 @@ __global__ __launch_bounds__(kBlock, 2) void KAesMmo(const uint4* in, uint4* out
   }
 }
 
+// EvaluateUntil's per-prefix roots (dpf.cc): prefix i
+// starts from the partial evaluation of its tree index (row idx[i] of
+// seeds / cb, written by the context walk) and walks `walk` (< 8, the
+// previous level's log2(elements per block)) more levels along the low bits
+// low[i] — the prefix's own node, which EvaluateUntil then expands.  Indices
+// come from the host and are in range by construction; they are clamped so a
+// corrupted one cannot read outside.
+__global__ __launch_bounds__(256, 2) void KPrefixRoots(int64_t n, const int32_t* idx,
+                                                       const uint8_t* low, int walk,
+                                                       int64_t num_src, const uint4* seeds,
+                                                       const uint8_t* cb, const uint4* cw_seed,
+                                                       const uint8_t* ccl, const uint8_t* ccr,
+                                                       uint4* seeds_out, uint8_t* cb_out) {
+  __shared__ uint32_t tab[kTabWords];
+  if (walk > 0) {  // kernel-uniform
+    FillTables(tab);
+    __syncthreads();
+  }
+  const Lds L = MakeLds(tab);
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
+    int64_t j = idx[i];
+    j = j < 0 ? 0 : j >= num_src ? num_src - 1 : j;
+    const uint4 s = seeds[j];
+    uint32_t x[4] = {s.x, s.y, s.z, s.w};
+    uint32_t t = cb[j];
+    const uint32_t bits = low[i];
+    for (int l = 0; l < walk; ++l) {
+      const uint32_t bit = (bits >> (walk - 1 - l)) & 1u;
+      WalkStep(x, t, bit, LoadCw(cw_seed, ccl, ccr, l), DpfMasked<1>{{0u - bit}}, L);
+    }
+    seeds_out[i] = make_uint4(x[0], x[1], x[2], x[3]);
+    cb_out[i] = (uint8_t)t;
+  }
+}
+
+int PrefixRoots(int64_t n, const int32_t* idx, const uint8_t* low, int walk, int64_t num_src,
+                const void* seeds, const uint8_t* cb, const void* cw_seed, const uint8_t* ccl,
+                const uint8_t* ccr, void* seeds_out, uint8_t* cb_out, void* stream) {
+  if (n <= 0) return DPF_AMD_OK;
+  if (num_src <= 0 || walk < 0 || walk > 7)
+    return SetError(DPF_AMD_INTERNAL, "bad prefix roots arguments");
+  const int grid = (int)std::min<int64_t>(1024, (n + 255) / 256);
+  hipLaunchKernelGGL(KPrefixRoots, dim3(grid), dim3(256), 0, (hipStream_t)stream, n, idx, low,
+                     walk, num_src, (const uint4*)seeds, cb, (const uint4*)cw_seed, ccl, ccr,
+                     (uint4*)seeds_out, cb_out);
+  return LaunchCheck("prefix roots kernel launch");
+}
+
 int LaunchEvaluateSeeds(int64_t n, hipStream_t st, const WalkArgs& a, const KeyPair& kp) {
   const int block = WalkBlock(n);
   const int grid = (int)std::min<int64_t>(DPF_WALK_MAX_GRID, (n + block - 1) / block);
