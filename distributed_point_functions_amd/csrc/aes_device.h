@@ -99,6 +99,8 @@ struct KeyNoPost {
 };
 template <int W>
 struct DpfKeyAt : KeyNoPost {  // one fixed DPF key for all states
+  // DPF_BS_LAST >= 2: the value PRG pairs' last round on the VALU too
+  static constexpr bool kBsLast = DPF_BS_LAST >= 2;
   __device__ __forceinline__ uint32_t rk(int, int i) const { return kDpfKeys[W].rk[i]; }
   __device__ __forceinline__ uint32_t rkr(int, int i) const { return kDpfKeys[W].rkr[i]; }
 };
