@@ -430,6 +430,9 @@ __device__ __forceinline__ void QuadWalkStep(uint32_t& x, uint32_t& t, uint32_t 
 #ifndef DPF_QUAD_RKM
 #define DPF_QUAD_RKM 1
 #endif
+#ifndef DPF_QUAD_POSTDPP
+#define DPF_QUAD_POSTDPP 0
+#endif
 constexpr int kTab4Words = 2 * kTabWords;  // 128 KiB
 
 __device__ __forceinline__ void FillTables4(uint32_t* tab) {
@@ -493,6 +496,29 @@ __device__ __forceinline__ uint32_t AesQuadRk(uint32_t w, const QuadRk& k, const
   w ^= k.rk[0];
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
+    if constexpr (T4 && DPF_QUAD_POSTDPP) {
+      // lookups on this lane's own bytes first, the moves after: lane c's
+      // T_k[byte k of column c] is what lane c - k needs.  The chain of a
+      // round is v_perm -> ds_read -> (3 DPP-sourced ops) -> xor3, one VALU
+      // level shorter than moving the column words before the lookups (and no
+      // VALU-write -> DPP-read wait states on w).
+      const uint32_t u0 = LoadT0(LdsOf(L), w, 0), u1 = LoadT1(LdsOf(L), w, 1),
+                     u2 = LoadT2(L, w, 2), u3 = LoadT3(L, w, 3);
+#if DPF_QUAD_POSTDPP >= 2
+      // the moves folded into the XORs' first operand (VOP2 DPP); u1 / u3
+      // come from ds_read, so no VALU-write -> DPP-read wait state applies
+      uint32_t a, b;
+      asm("v_xor_b32_dpp %0, %1, %2 quad_perm:[1,2,3,0] row_mask:0xf bank_mask:0xf"
+          : "=v"(a) : "v"(u1), "v"(u0));
+      asm("v_xor_b32_dpp %0, %1, %2 quad_perm:[3,0,1,2] row_mask:0xf bank_mask:0xf"
+          : "=v"(b) : "v"(u3), "v"(k.rk[r]));
+#else
+      const uint32_t a = QuadPerm<kQuadNext1>(u1) ^ u0;
+      const uint32_t b = QuadPerm<kQuadNext3>(u3) ^ k.rk[r];
+#endif
+      w = Xor3(a, b, QuadPerm<kQuadNext2>(u2));
+      continue;
+    }
     const uint32_t x1 = QuadPerm<kQuadNext1>(w), x2 = QuadPerm<kQuadNext2>(w),
                    x3 = QuadPerm<kQuadNext3>(w);
     if constexpr (T4) {
