@@ -431,7 +431,7 @@ __device__ __forceinline__ void QuadWalkStep(uint32_t& x, uint32_t& t, uint32_t 
 #define DPF_QUAD_RKM 1
 #endif
 #ifndef DPF_QUAD_POSTDPP
-#define DPF_QUAD_POSTDPP 0
+#define DPF_QUAD_POSTDPP 1
 #endif
 constexpr int kTab4Words = 2 * kTabWords;  // 128 KiB
 
