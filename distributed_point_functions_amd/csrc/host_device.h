@@ -324,6 +324,23 @@ inline size_t D2HDirectMax() {
   return v;
 }
 
+// How a thread waits for its D2H copies: hipEventSynchronize, or
+// (DPF_AMD_SPIN_WAIT=1) polling hipEventQuery — a synchronous API call whose
+// thread is blocked anyway trades a core for the wake-up latency.
+inline bool SpinWait() {
+  static const bool v = [] {
+    const char* e = std::getenv("DPF_AMD_SPIN_WAIT");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
+  return v;
+}
+inline hipError_t WaitEvent(hipEvent_t ev) {
+  if (!SpinWait()) return hipEventSynchronize(ev);
+  hipError_t e;
+  while ((e = hipEventQuery(ev)) == hipErrorNotReady) __builtin_ia32_pause();
+  return e;
+}
+
 // Device-to-host copy into pageable `dst`, complete on return.  A plain
 // hipMemcpy into pageable memory stages through the runtime's own small
 // pinned buffers one after the other; copies above 1 MiB here go through two
@@ -371,7 +388,7 @@ class D2HStaging {
       }
       if (i >= 1) {
         const size_t j = i - 1;
-        DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(ev_[j & 1]), "d2h"));
+        DPF_RETURN_IF_ERROR(HipStatus(WaitEvent(ev_[j & 1]), "d2h"));
         HostPool::Get().Copy(dst + j * kChunk, static_cast<const char*>(pin_[j & 1]), len(j));
       }
     }
@@ -446,7 +463,7 @@ class H2DStaging {
 inline H2DStaging& ThreadH2DStaging() { return ThreadRecycled<H2DStaging>::Get(); }
 
 inline Status CopyToHostSync(void* dst, const void* src, size_t bytes, hipStream_t s) {
-  if (bytes <= D2HDirectMax()) {
+  if (bytes <= D2HDirectMax() && !SpinWait()) {
     DPF_RETURN_IF_ERROR(CopyToHost(dst, src, bytes, s));
     return HipStatus(hipStreamSynchronize(s), "sync");
   }
