@@ -1751,20 +1751,38 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
     const size_t out_off = bi_off + (m.epb > 1 ? ((size_t(n) + 15) & ~size_t{15}) : 0);
     DeviceBuffer buf;
     trace.Mark("prepare");
-    DPF_RETURN_IF_ERROR(buf.Alloc(out_off + size_t(n) * vt.out_stride, s));
+    const size_t out_bytes = size_t(n) * vt.out_stride;
+    const bool host_out = out_bytes <= dpf_internal_host::HostOutMax();
+    void* hout = nullptr;
+    void* kout = nullptr;
+    if (host_out)
+      DPF_RETURN_IF_ERROR(
+          dpf_internal_host::ThreadRecycled<dpf_internal_host::PinnedOut>::Get().Get(
+              out_bytes, &hout, &kout));
+    DPF_RETURN_IF_ERROR(buf.Alloc(out_off + (host_out ? 0 : out_bytes), s));
     char* d = buf.as<char>();
+    if (!host_out) kout = d + out_off;
     DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 6, in_bytes, off, s));
     if (m.epb > 1) DPF_RETURN_IF_ERROR(ThreadUploadRing().Copy(d + bi_off, bidx, n, s));
-    DPF_RETURN_IF_ERROR(ClearPadding(vt, d + out_off, n * vt.out_stride, s));
+    if (host_out) {
+      if (dpf_internal_host::HasPadding(vt)) std::memset(hout, 0, out_bytes);
+    } else {
+      DPF_RETURN_IF_ERROR(ClearPadding(vt, kout, out_bytes, s));
+    }
     trace.Mark("alloc+upload");
     DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_points_batched(
         1, n, d + off[1], reinterpret_cast<const uint8_t*>(d + off[5]), d + off[0], 0, levels,
         d + off[2], reinterpret_cast<const uint8_t*>(d + off[3]),
         reinterpret_cast<const uint8_t*>(d + off[4]), &vt,
         m.epb > 1 ? reinterpret_cast<const uint8_t*>(d + bi_off) : nullptr, nullptr,
-        key.party(), nullptr, reinterpret_cast<const uint64_t*>(corr.data()), d + out_off, s)));
+        key.party(), nullptr, reinterpret_cast<const uint64_t*>(corr.data()), kout, s)));
     trace.Mark("launch");
-    DPF_RETURN_IF_ERROR(CopyToHostSync(out, d + out_off, n * vt.out_stride, s));
+    if (host_out) {
+      DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+      std::memcpy(out, hout, out_bytes);
+    } else {
+      DPF_RETURN_IF_ERROR(CopyToHostSync(out, kout, out_bytes, s));
+    }
     trace.Mark("d2h+sync");
     return OkStatus();
   }

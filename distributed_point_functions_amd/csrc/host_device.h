@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <thread>
@@ -253,13 +254,14 @@ class HostPool {
       job_ = job;
       next_ = 1;
       parts_ = parts;
-      pending_ = parts - 1;
-      ++gen_;
+      pending_.store(parts - 1, std::memory_order_relaxed);
+      gen_.fetch_add(1, std::memory_order_release);
     }
     cv_.notify_all();
     fn(size_t{0});  // part 0 on the caller
+    if (SpinUntil([&] { return pending_.load(std::memory_order_acquire) == 0; })) return;
     std::unique_lock<std::mutex> l(mu_);
-    done_cv_.wait(l, [&] { return pending_ == 0; });
+    done_cv_.wait(l, [&] { return pending_.load(std::memory_order_relaxed) == 0; });
   }
   // Splits [0, n) into at most kWorkers + 1 ranges of at least `grain`.
   // Returns the number of ranges (range i is fn's first argument).
@@ -291,27 +293,52 @@ class HostPool {
   HostPool() {
     for (size_t i = 0; i < kWorkers; ++i) std::thread([this] { Work(); }).detach();
   }
+  // Bounded busy-wait before a futex sleep (DPF_AMD_POOL_SPIN_US, default
+  // 0 = sleep at once): the incremental path issues several short Runs per
+  // call, where a sleeping worker's wake-up rivals the part's work.
+  static int64_t SpinNs() {
+    static const int64_t v = [] {
+      const char* e = std::getenv("DPF_AMD_POOL_SPIN_US");
+      return e ? std::max<int64_t>(0, std::atoll(e)) * 1000 : int64_t{0};
+    }();
+    return v;
+  }
+  template <typename Pred>
+  static bool SpinUntil(const Pred& pred) {
+    const int64_t ns = SpinNs();
+    if (ns == 0) return pred();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0;; ++k) {
+      if (pred()) return true;
+      if ((k & 63) == 63 && std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                std::chrono::steady_clock::now() - t0).count() > ns)
+        return pred();
+      __builtin_ia32_pause();
+    }
+  }
   void Work() {
     uint64_t seen = 0;
     for (;;) {
+      SpinUntil([&] { return gen_.load(std::memory_order_acquire) != seen; });
       std::unique_lock<std::mutex> l(mu_);
-      cv_.wait(l, [&] { return gen_ != seen && next_ < parts_; });
-      seen = gen_;
+      cv_.wait(l, [&] { return gen_.load(std::memory_order_relaxed) != seen; });
+      seen = gen_.load(std::memory_order_relaxed);  // a job fully taken already: back to waiting
       while (next_ < parts_) {
         const size_t i = next_++;
         const Job job = job_;
         l.unlock();
         job.call(job.fn, i);
         l.lock();
-        if (--pending_ == 0) done_cv_.notify_one();
+        if (pending_.fetch_sub(1, std::memory_order_acq_rel) == 1) done_cv_.notify_one();
       }
     }
   }
   std::mutex call_mu_, mu_;
   std::condition_variable cv_, done_cv_;
   Job job_{nullptr, nullptr};
-  size_t next_ = 0, parts_ = 0, pending_ = 0;
-  uint64_t gen_ = 0;
+  size_t next_ = 0, parts_ = 0;
+  std::atomic<size_t> pending_{0};
+  std::atomic<uint64_t> gen_{0};
 };
 
 // Largest D2H copy into pageable memory left to the runtime's own path
@@ -324,22 +351,49 @@ inline size_t D2HDirectMax() {
   return v;
 }
 
-// How a thread waits for its D2H copies: hipEventSynchronize, or
-// (DPF_AMD_SPIN_WAIT=1) polling hipEventQuery — a synchronous API call whose
-// thread is blocked anyway trades a core for the wake-up latency.
-inline bool SpinWait() {
-  static const bool v = [] {
-    const char* e = std::getenv("DPF_AMD_SPIN_WAIT");
-    return e != nullptr && std::atoi(e) != 0;
+// Small results written by the kernel straight into pinned host memory
+// (DPF_AMD_HOST_OUT_KB, default 0 = off): one EvaluateAt's outputs then
+// reach the host without a copy-engine transfer and its completion wait —
+// the kernel's stores cross PCIe as it retires, and the call copies the
+// block into the caller's buffer after one stream sync.
+inline size_t HostOutMax() {
+  static const size_t v = [] {
+    const char* e = std::getenv("DPF_AMD_HOST_OUT_KB");
+    return (e ? std::strtoull(e, nullptr, 10) : 0ull) << 10;
   }();
   return v;
 }
-inline hipError_t WaitEvent(hipEvent_t ev) {
-  if (!SpinWait()) return hipEventSynchronize(ev);
-  hipError_t e;
-  while ((e = hipEventQuery(ev)) == hipErrorNotReady) __builtin_ia32_pause();
-  return e;
-}
+class PinnedOut {
+ public:
+  PinnedOut() = default;
+  PinnedOut(const PinnedOut&) = delete;
+  PinnedOut& operator=(const PinnedOut&) = delete;
+  ~PinnedOut() {
+    if (p_) (void)hipHostFree(p_);
+  }
+  // A block of at least `bytes` (host pointer, and the pointer kernels
+  // write through); the previous user has synchronized.
+  Status Get(size_t bytes, void** host, void** dev) {
+    if (cap_ < bytes) {
+      if (p_) (void)hipHostFree(p_);
+      p_ = d_ = nullptr;
+      cap_ = 0;
+      size_t cap = 64u << 10;
+      while (cap < bytes) cap <<= 1;
+      DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc(&p_, cap, hipHostMallocMapped), "hipHostMalloc"));
+      DPF_RETURN_IF_ERROR(HipStatus(hipHostGetDevicePointer(&d_, p_, 0), "hipHostGetDevicePointer"));
+      cap_ = cap;
+    }
+    *host = p_;
+    *dev = d_;
+    return OkStatus();
+  }
+
+ private:
+  void* p_ = nullptr;
+  void* d_ = nullptr;
+  size_t cap_ = 0;
+};
 
 // Device-to-host copy into pageable `dst`, complete on return.  A plain
 // hipMemcpy into pageable memory stages through the runtime's own small
@@ -388,7 +442,7 @@ class D2HStaging {
       }
       if (i >= 1) {
         const size_t j = i - 1;
-        DPF_RETURN_IF_ERROR(HipStatus(WaitEvent(ev_[j & 1]), "d2h"));
+        DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(ev_[j & 1]), "d2h"));
         HostPool::Get().Copy(dst + j * kChunk, static_cast<const char*>(pin_[j & 1]), len(j));
       }
     }
@@ -463,7 +517,7 @@ class H2DStaging {
 inline H2DStaging& ThreadH2DStaging() { return ThreadRecycled<H2DStaging>::Get(); }
 
 inline Status CopyToHostSync(void* dst, const void* src, size_t bytes, hipStream_t s) {
-  if (bytes <= D2HDirectMax() && !SpinWait()) {
+  if (bytes <= D2HDirectMax()) {
     DPF_RETURN_IF_ERROR(CopyToHost(dst, src, bytes, s));
     return HipStatus(hipStreamSynchronize(s), "sync");
   }
