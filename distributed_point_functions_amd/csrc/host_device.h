@@ -6,7 +6,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <thread>
@@ -254,14 +253,13 @@ class HostPool {
       job_ = job;
       next_ = 1;
       parts_ = parts;
-      pending_.store(parts - 1, std::memory_order_relaxed);
-      gen_.fetch_add(1, std::memory_order_release);
+      pending_ = parts - 1;
+      ++gen_;
     }
     cv_.notify_all();
     fn(size_t{0});  // part 0 on the caller
-    if (SpinUntil([&] { return pending_.load(std::memory_order_acquire) == 0; })) return;
     std::unique_lock<std::mutex> l(mu_);
-    done_cv_.wait(l, [&] { return pending_.load(std::memory_order_relaxed) == 0; });
+    done_cv_.wait(l, [&] { return pending_ == 0; });
   }
   // Splits [0, n) into at most kWorkers + 1 ranges of at least `grain`.
   // Returns the number of ranges (range i is fn's first argument).
@@ -293,52 +291,27 @@ class HostPool {
   HostPool() {
     for (size_t i = 0; i < kWorkers; ++i) std::thread([this] { Work(); }).detach();
   }
-  // Bounded busy-wait before a futex sleep (DPF_AMD_POOL_SPIN_US, default
-  // 0 = sleep at once): the incremental path issues several short Runs per
-  // call, where a sleeping worker's wake-up rivals the part's work.
-  static int64_t SpinNs() {
-    static const int64_t v = [] {
-      const char* e = std::getenv("DPF_AMD_POOL_SPIN_US");
-      return e ? std::max<int64_t>(0, std::atoll(e)) * 1000 : int64_t{0};
-    }();
-    return v;
-  }
-  template <typename Pred>
-  static bool SpinUntil(const Pred& pred) {
-    const int64_t ns = SpinNs();
-    if (ns == 0) return pred();
-    const auto t0 = std::chrono::steady_clock::now();
-    for (int k = 0;; ++k) {
-      if (pred()) return true;
-      if ((k & 63) == 63 && std::chrono::duration_cast<std::chrono::nanoseconds>(
-                                std::chrono::steady_clock::now() - t0).count() > ns)
-        return pred();
-      __builtin_ia32_pause();
-    }
-  }
   void Work() {
     uint64_t seen = 0;
     for (;;) {
-      SpinUntil([&] { return gen_.load(std::memory_order_acquire) != seen; });
       std::unique_lock<std::mutex> l(mu_);
-      cv_.wait(l, [&] { return gen_.load(std::memory_order_relaxed) != seen; });
-      seen = gen_.load(std::memory_order_relaxed);  // a job fully taken already: back to waiting
+      cv_.wait(l, [&] { return gen_ != seen && next_ < parts_; });
+      seen = gen_;
       while (next_ < parts_) {
         const size_t i = next_++;
         const Job job = job_;
         l.unlock();
         job.call(job.fn, i);
         l.lock();
-        if (pending_.fetch_sub(1, std::memory_order_acq_rel) == 1) done_cv_.notify_one();
+        if (--pending_ == 0) done_cv_.notify_one();
       }
     }
   }
   std::mutex call_mu_, mu_;
   std::condition_variable cv_, done_cv_;
   Job job_{nullptr, nullptr};
-  size_t next_ = 0, parts_ = 0;
-  std::atomic<size_t> pending_{0};
-  std::atomic<uint64_t> gen_{0};
+  size_t next_ = 0, parts_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
 };
 
 // Largest D2H copy into pageable memory left to the runtime's own path
@@ -352,14 +325,14 @@ inline size_t D2HDirectMax() {
 }
 
 // Small results written by the kernel straight into pinned host memory
-// (DPF_AMD_HOST_OUT_KB, default 0 = off): one EvaluateAt's outputs then
+// (up to DPF_AMD_HOST_OUT_KB, default 1024): one EvaluateAt's outputs then
 // reach the host without a copy-engine transfer and its completion wait —
 // the kernel's stores cross PCIe as it retires, and the call copies the
 // block into the caller's buffer after one stream sync.
 inline size_t HostOutMax() {
   static const size_t v = [] {
     const char* e = std::getenv("DPF_AMD_HOST_OUT_KB");
-    return (e ? std::strtoull(e, nullptr, 10) : 0ull) << 10;
+    return (e ? std::strtoull(e, nullptr, 10) : 1024ull) << 10;
   }();
   return v;
 }
