@@ -353,7 +353,8 @@ class PinnedOut {
       cap_ = 0;
       size_t cap = 64u << 10;
       while (cap < bytes) cap <<= 1;
-      DPF_RETURN_IF_ERROR(HipStatus(hipHostMalloc(&p_, cap, hipHostMallocMapped), "hipHostMalloc"));
+      DPF_RETURN_IF_ERROR(HipStatus(
+          hipHostMalloc(&p_, cap, hipHostMallocMapped | hipHostMallocPortable), "hipHostMalloc"));
       DPF_RETURN_IF_ERROR(HipStatus(hipHostGetDevicePointer(&d_, p_, 0), "hipHostGetDevicePointer"));
       cap_ = cap;
     }
