@@ -1225,6 +1225,7 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
       });
       for (int r = 0; r < parts; ++r) merged &= ok[r];
     }
+    trace.Mark("stored_order");
     if (merged && n > 0) {
       const int parts = pool.ParallelRanges(n, 4096, [&](int r, int64_t b, int64_t e) {
         ok[r] = true;
@@ -1386,31 +1387,54 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
         "`prefixes` must be empty if and only if this is the first call with `ctx`.");
   int previous_log_domain_size = 0;
   const int prev_h = ctx.previous_hierarchy_level();
-  if (!prefixes.empty()) {
-    previous_log_domain_size = st.parameters[prev_h].log_domain_size();
+  // The prefixes' range check (h:735-745): the first prefix out of range is
+  // the error, and it precedes every later one.  Large prefix lists are
+  // checked inside the de-duplication's first parallel pass instead of a
+  // serial loop of their own; every error return before that pass runs the
+  // serial check first, so the reported error is the reference's.
+  if (!prefixes.empty()) previous_log_domain_size = st.parameters[prev_h].log_domain_size();
+  const uint128 prefix_limit = previous_log_domain_size < 128
+                                   ? (uint128{1} << previous_log_domain_size)
+                                   : uint128{0};  // 0: every prefix is in range
+  auto range_check = [&]() -> Status {
+    if (prefix_limit == 0) return OkStatus();
     for (uint128 p : prefixes)
-      if (previous_log_domain_size < 128 && p >= (uint128{1} << previous_log_domain_size))
+      if (p >= prefix_limit)
         return InvalidArgumentError("Index " + dpf_internal::U128ToString(p) +
                                     " out of range for hierarchy level " + std::to_string(prev_h));
-  }
+    return OkStatus();
+  };
+  const bool range_deferred =
+      out != nullptr && static_cast<int64_t>(prefixes.size()) >= (int64_t{1} << 14);
+  if (!range_deferred) DPF_RETURN_IF_ERROR(range_check());
+  auto early = [&](Status e) -> Status {
+    if (range_deferred) DPF_RETURN_IF_ERROR(range_check());
+    return e;
+  };
   trace.Mark("range_check");
   const int log_domain_size = st.parameters[hierarchy_level].log_domain_size();
   if (log_domain_size - previous_log_domain_size > 62)
-    return InvalidArgumentError(
+    return early(InvalidArgumentError(
         "Output size would be larger than 2**62. Please evaluate fewer hierarchy levels at "
-        "once.");
+        "once."));
   const int64_t num_prefixes = static_cast<int64_t>(prefixes.size());
   const int64_t outputs_per_prefix = int64_t{1} << (log_domain_size - previous_log_domain_size);
   const int64_t total = prefixes.empty() ? outputs_per_prefix : num_prefixes * outputs_per_prefix;
   *num_outputs = total;
   if (out == nullptr) return OkStatus();
-  if (out_capacity < total) return InvalidArgumentError("output buffer too small");
+  if (out_capacity < total) return early(InvalidArgumentError("output buffer too small"));
 
   const LevelMeta& m = st.levels[hierarchy_level];
   dpf_amd_value_type vt;
-  DPF_RETURN_IF_ERROR(MergeLayout(m, layout, &vt));
+  {
+    Status e = MergeLayout(m, layout, &vt);
+    if (!e.ok()) return early(e);
+  }
   std::vector<uint128> corr;
-  DPF_RETURN_IF_ERROR(CorrectionsFor(st, ctx.key(), hierarchy_level, &corr));
+  {
+    Status e = CorrectionsFor(st, ctx.key(), hierarchy_level, &corr);
+    if (!e.ok()) return early(e);
+  }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ThreadStream();
   trace.Mark("corrections");
 
@@ -1421,8 +1445,14 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   // the reference's btree.
   IncrementalScratch& sc = ThreadScratch();
   // a DMA an earlier call left in flight into the scratch must have landed
-  if (sc.done) DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(sc.done), "d2h"));
-  DPF_RETURN_IF_ERROR(sc.Reserve(num_prefixes > 0 ? num_prefixes : 1));
+  if (sc.done) {
+    Status e = HipStatus(hipEventSynchronize(sc.done), "d2h");
+    if (!e.ok()) return early(e);
+  }
+  {
+    Status e = sc.Reserve(num_prefixes > 0 ? num_prefixes : 1);
+    if (!e.ok()) return early(e);
+  }
   uint128* tree_indices = sc.tree;
   std::vector<int64_t>& src = sc.src;
   int64_t num_unique = 0;
@@ -1449,12 +1479,14 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
     if (!fused && static_cast<int64_t>(src.size()) < num_prefixes) src.resize(num_prefixes);
     constexpr int kParts = static_cast<int>(HostPool::kWorkers) + 1;
     int64_t count[kParts] = {}, first[kParts] = {};
-    bool ordered[kParts];
+    bool ordered[kParts], in_range[kParts];
     HostPool& pool = HostPool::Get();
+    const uint128 lim = prefix_limit;
     const int parts = pool.ParallelRanges(num_prefixes, 8192, [&](int r, int64_t b, int64_t e) {
-      bool ok = true;
+      bool ok = true, inr = true;
       int64_t u = 0;
       for (int64_t i = b; i < e; ++i) {
+        inr &= lim == 0 || prefixes[i] < lim;
         if (i == 0) {
           ++u;
           continue;
@@ -1463,14 +1495,18 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
         u += (prefixes[i] >> bbits) != (prefixes[i - 1] >> bbits);
       }
       ordered[r] = ok;
+      in_range[r] = inr;
       count[r] = u;
     });
-    bool sorted = true;
+    bool sorted = true, all_in_range = true;
     for (int r = 0; r < parts; ++r) {
       sorted &= ordered[r];
+      all_in_range &= in_range[r];
       first[r] = num_unique;
       num_unique += count[r];
     }
+    if (!all_in_range) return range_check();  // the reference's message for the first one
+    trace.Mark("dedup_count");
     if (sorted) {
       pool.ParallelRanges(num_prefixes, 8192, [&](int r, int64_t b, int64_t e) {
         int64_t u = first[r];

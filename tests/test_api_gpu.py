@@ -422,6 +422,42 @@ def test_incremental_unsorted_duplicate_and_missing_prefixes(api):
     assert str(ours.value).split(":")[-1].strip() == str(ref.value).split(":")[-1].strip()
 
 
+@pytest.mark.parametrize("n", [100, 1 << 14])
+def test_incremental_prefix_range_error_names_the_first_bad_prefix(api, n):
+    """EvaluateUntil's prefix range check (h:735-745): the first prefix at or
+    above 2^previous_log_domain_size is reported with the reference's message,
+    for short lists (checked up front) and long ones (checked inside the
+    de-duplication's parallel pass), and the context is left untouched so the
+    same level still evaluates afterwards."""
+    D, V, _ = api
+    spec = ("int", 64)
+    levels = [(ld, spec, 40 + ld) for ld in (8, 16)]
+    rng = random.Random(79)
+    alpha, betas = rng.getrandbits(16), [rng.getrandbits(64) for _ in range(2)]
+    seeds = (rng.getrandbits(128), rng.getrandbits(128))
+    dpf = _make(api, levels)
+    od = po.Dpf(levels)
+    k0, _ = dpf.generate_keys_incremental(alpha, betas, seeds=seeds)
+    ok0, _ = od.generate_keys(alpha, betas, seeds=seeds)
+    vt = V.from_spec(spec)
+    ctx = dpf.create_evaluation_context(k0)
+    octx = od.create_evaluation_context(ok0)
+    dpf.evaluate_next([], ctx, raw=True)
+    od.evaluate_until(0, [], octx)
+    good = sorted(rng.randrange(256) for _ in range(n))
+    bad = list(good)
+    bad[n // 3] = 300
+    bad[2 * n // 3] = 999
+    with pytest.raises(Exception) as ours:
+        dpf.evaluate_next(bad, ctx, raw=True)
+    with pytest.raises(Exception) as ref:
+        od.evaluate_until(1, bad, octx)
+    assert "Index 300 out of range for hierarchy level 0" in str(ours.value)
+    assert str(ours.value).split(":")[-1].strip() == str(ref.value).split(":")[-1].strip()
+    got = vt.decode_flat(dpf.evaluate_next(good, ctx, raw=True))
+    assert got == od.evaluate_until(1, good, octx)
+
+
 def test_incremental_duplicate_partial_evaluation_past_the_queries(api):
     """A duplicate stored prefix with a mismatching seed is rejected wherever
     it sits in ctx.partial_evaluations (cc:390-405 builds its btree from the
