@@ -1140,6 +1140,26 @@ IncrementalScratch& ThreadScratch() {
 // seeds come back by DMA behind the walk, and the caller rewrites `ctx`
 // (FinishContextUpdate) after it has queued the expansion, so the host work
 // overlaps the GPU's.
+// ctx.partial_evaluations = (prefix i, seed i, control bit i), the stored
+// list of cc:505-519.  The list is resized in place (the previous level's
+// entries are overwritten, not destroyed and value-initialised again) and
+// filled over the host pool: 2^16 entries per c3 level.
+void RewritePartialEvaluations(EvaluationContext& ctx, const uint128* prefixes,
+                               const uint128* seeds, const uint8_t* cbs, int64_t n) {
+  std::vector<PartialEvaluation>* pe = ctx.mutable_partial_evaluations();
+  pe->resize(n);
+  HostPool::Get().ParallelRanges(n, 8192, [&](int, int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i) {
+      PartialEvaluation& x = (*pe)[i];
+      x.mutable_prefix()->set_high(Uint128High64(prefixes[i]));
+      x.mutable_prefix()->set_low(Uint128Low64(prefixes[i]));
+      x.mutable_seed()->set_high(Uint128High64(seeds[i]));
+      x.mutable_seed()->set_low(Uint128Low64(seeds[i]));
+      x.set_control_bit(cbs[i] != 0);
+    }
+  });
+}
+
 struct PendingContextUpdate {
   bool active = false;
   Span<const uint128> prefixes;
@@ -1153,17 +1173,8 @@ Status FinishContextUpdate(PendingContextUpdate& p, EvaluationContext& ctx) {
   IncrementalScratch& sc = ThreadScratch();
   DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(sc.done), "d2h"));
   trace.Mark("wait");
-  const int64_t n = static_cast<int64_t>(p.prefixes.size());
-  std::vector<PartialEvaluation>* pe = ctx.mutable_partial_evaluations();
-  pe->resize(n);
-  for (int64_t i = 0; i < n; ++i) {
-    PartialEvaluation& e = (*pe)[i];
-    e.mutable_prefix()->set_high(Uint128High64(p.prefixes[i]));
-    e.mutable_prefix()->set_low(Uint128Low64(p.prefixes[i]));
-    e.mutable_seed()->set_high(Uint128High64(sc.seeds[i]));
-    e.mutable_seed()->set_low(Uint128Low64(sc.seeds[i]));
-    e.set_control_bit(sc.cbs[i] != 0);
-  }
+  RewritePartialEvaluations(ctx, p.prefixes.data(), sc.seeds, sc.cbs,
+                            static_cast<int64_t>(p.prefixes.size()));
   ctx.set_partial_evaluations_level(p.hierarchy_level);
   trace.Mark("rewrite");
   return OkStatus();
@@ -1217,49 +1228,51 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
     constexpr int kParts = static_cast<int>(HostPool::kWorkers) + 1;
     bool ok[kParts];
     if (merged) {
-      const int parts = pool.ParallelRanges(m, 8192, [&](int r, int64_t b, int64_t e) {
+      // One pool job: part r checks the strict order of its slice of the
+      // stored list and merges its slice of the queries.
+      const int64_t parts = std::max<int64_t>(
+          1, std::min<int64_t>(kParts, std::max(n / 4096, m / 8192)));
+      const int64_t mper = (m + parts - 1) / parts, nper = (n + parts - 1) / parts;
+      pool.Run(static_cast<size_t>(parts), [&](size_t r) {
         bool good = true;
-        for (int64_t k = std::max<int64_t>(b, 1); k < e; ++k)
+        const int64_t mb = std::min<int64_t>(static_cast<int64_t>(r) * mper, m),
+                      me = std::min<int64_t>(mb + mper, m);
+        for (int64_t k = std::max<int64_t>(mb, 1); k < me; ++k)
           good &= pe_prefix(k - 1) < pe_prefix(k);
-        ok[r] = good;
-      });
-      for (int r = 0; r < parts; ++r) merged &= ok[r];
-    }
-    trace.Mark("stored_order");
-    if (merged && n > 0) {
-      const int parts = pool.ParallelRanges(n, 4096, [&](int r, int64_t b, int64_t e) {
-        ok[r] = true;
-        if (b >= e) return;
-        bool good = b == 0 || query(b - 1) <= query(b);
-        const uint128 q0 = query(b);
-        int64_t lo = 0, hi = m;  // first stored prefix >= q0
-        while (lo < hi) {
-          const int64_t mid = lo + (hi - lo) / 2;
-          if (pe_prefix(mid) < q0)
-            lo = mid + 1;
-          else
-            hi = mid;
-        }
-        int64_t j = lo;
-        uint128 prev = q0;
-        for (int64_t i = b; i < e && good; ++i) {
-          const uint128 q = query(i);
-          if (q < prev) {
-            good = false;
-            break;
+        const int64_t b = std::min<int64_t>(static_cast<int64_t>(r) * nper, n),
+                      e = std::min<int64_t>(b + nper, n);
+        if (good && b < e) {
+          good = b == 0 || query(b - 1) <= query(b);
+          const uint128 q0 = query(b);
+          int64_t lo = 0, hi = m;  // first stored prefix >= q0
+          while (lo < hi) {
+            const int64_t mid = lo + (hi - lo) / 2;
+            if (pe_prefix(mid) < q0)
+              lo = mid + 1;
+            else
+              hi = mid;
           }
-          prev = q;
-          while (j < m && pe_prefix(j) < q) ++j;
-          if (j == m || pe_prefix(j) != q) {
-            good = false;
-            break;
+          int64_t j = lo;
+          uint128 prev = q0;
+          for (int64_t i = b; i < e && good; ++i) {
+            const uint128 q = query(i);
+            if (q < prev) {
+              good = false;
+              break;
+            }
+            prev = q;
+            while (j < m && pe_prefix(j) < q) ++j;
+            if (j == m || pe_prefix(j) != q) {
+              good = false;
+              break;
+            }
+            seeds[i] = MakeUint128(pes[j].seed().high(), pes[j].seed().low());
+            cbs[i] = pes[j].control_bit() ? 1 : 0;
           }
-          seeds[i] = MakeUint128(pes[j].seed().high(), pes[j].seed().low());
-          cbs[i] = pes[j].control_bit() ? 1 : 0;
         }
         ok[r] = good;
       });
-      for (int r = 0; r < parts; ++r) merged &= ok[r];
+      for (int64_t r = 0; r < parts; ++r) merged &= ok[r];
     }
     if (!merged) {
       std::unordered_map<uint128, std::pair<uint128, bool>, U128Hash> prev;
@@ -1333,7 +1346,7 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
         dpf_amd::kPrgKeyRightHi, d + off[0], *cb_dev, s)));
   }
   trace.Mark("upload+walk_launch");
-  ctx.clear_partial_evaluations();
+  if (!(update_ctx && n > 0)) ctx.clear_partial_evaluations();
   if (update_ctx && n > 0) {
     // seeds / cbs are pinned: the copies are true DMAs behind the walk
     DPF_RETURN_IF_ERROR(CopyToHost(seeds, *seeds_dev, 16 * n, s));
@@ -1347,16 +1360,7 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
       return OkStatus();
     }
     DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(sc.done), "sync"));
-    std::vector<PartialEvaluation>* pe = ctx.mutable_partial_evaluations();
-    pe->resize(n);
-    for (int64_t i = 0; i < n; ++i) {
-      PartialEvaluation& e = (*pe)[i];
-      e.mutable_prefix()->set_high(Uint128High64(prefixes[i]));
-      e.mutable_prefix()->set_low(Uint128Low64(prefixes[i]));
-      e.mutable_seed()->set_high(Uint128High64(seeds[i]));
-      e.mutable_seed()->set_low(Uint128Low64(seeds[i]));
-      e.set_control_bit(cbs[i] != 0);
-    }
+    RewritePartialEvaluations(ctx, prefixes.data(), seeds, cbs, n);
   }
   trace.Mark("d2h+ctx_rewrite");
   ctx.set_partial_evaluations_level(hierarchy_level);
