@@ -2,7 +2,10 @@
 // the LDS T-table AES (HashWords<1, 2, true>, the fused kernel's current leaf
 // hash) against the generated bitsliced AES (bsaes_gen.h, 16 pairs per lane).
 // Checks that both produce identical words, then times each over a large
-// grid.  Built and run by tools/run_bsaes_bench.sh; not part of the library.
+// grid.  Not part of the library: generate bsaes_gen.h first
+// (python tools/experiments/gen_bsaes.py), then
+//   hipcc --offload-arch=gfx950 -O3 -I distributed_point_functions_amd/csrc \
+//     -I include tools/experiments/bsaes_bench.hip -o bsaes_bench
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

@@ -5,7 +5,10 @@ function.cc:55-60, kPrgKeyValue) compiled into the circuit, 32 blocks per
 lane (one block per bit of a 32-bit VGPR), expressed in v_bitop3_b32
 (any 3-input boolean function in one VALU op) and v_perm_b32.
 
-    python tools/gen_bsaes.py            # writes the header, verifies it
+    python tools/experiments/gen_bsaes.py   # writes the header, verifies it
+
+(The header is generated, ~1.5 MB, and not kept in git: run this before
+building tools/experiments/bsaes_bench.hip.)
 
 Why: the T-table AES of the fused expansion kernel is bound by LDS lookup
 issue (~90 % of LDS-array cycles) while the VALU idles at ~45 % (DESIGN.md
