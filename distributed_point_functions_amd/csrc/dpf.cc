@@ -1160,6 +1160,10 @@ void RewritePartialEvaluations(EvaluationContext& ctx, const uint128* prefixes,
   });
 }
 
+#ifndef DPF_HOST_FUSED_LOOKUP
+#define DPF_HOST_FUSED_LOOKUP 1  // stored-order check and merge join in one pool job
+#endif
+
 struct PendingContextUpdate {
   bool active = false;
   Span<const uint128> prefixes;
@@ -1227,6 +1231,39 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
     HostPool& pool = HostPool::Get();
     constexpr int kParts = static_cast<int>(HostPool::kWorkers) + 1;
     bool ok[kParts];
+    // queries [b, e) against the stored list; false when the merge cannot
+    // decide (an order violation or a prefix not found)
+    auto merge_range = [&](int64_t b, int64_t e) {
+      if (b >= e) return true;
+      bool good = b == 0 || query(b - 1) <= query(b);
+      const uint128 q0 = query(b);
+      int64_t lo = 0, hi = m;  // first stored prefix >= q0
+      while (lo < hi) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (pe_prefix(mid) < q0)
+          lo = mid + 1;
+        else
+          hi = mid;
+      }
+      int64_t j = lo;
+      uint128 prev = q0;
+      for (int64_t i = b; i < e && good; ++i) {
+        const uint128 q = query(i);
+        if (q < prev) return false;
+        prev = q;
+        while (j < m && pe_prefix(j) < q) ++j;
+        if (j == m || pe_prefix(j) != q) return false;
+        seeds[i] = MakeUint128(pes[j].seed().high(), pes[j].seed().low());
+        cbs[i] = pes[j].control_bit() ? 1 : 0;
+      }
+      return good;
+    };
+    auto stored_order = [&](int64_t b, int64_t e) {
+      bool good = true;
+      for (int64_t k = std::max<int64_t>(b, 1); k < e; ++k) good &= pe_prefix(k - 1) < pe_prefix(k);
+      return good;
+    };
+#if DPF_HOST_FUSED_LOOKUP
     if (merged) {
       // One pool job: part r checks the strict order of its slice of the
       // stored list and merges its slice of the queries.
@@ -1234,46 +1271,25 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
           1, std::min<int64_t>(kParts, std::max(n / 4096, m / 8192)));
       const int64_t mper = (m + parts - 1) / parts, nper = (n + parts - 1) / parts;
       pool.Run(static_cast<size_t>(parts), [&](size_t r) {
-        bool good = true;
-        const int64_t mb = std::min<int64_t>(static_cast<int64_t>(r) * mper, m),
-                      me = std::min<int64_t>(mb + mper, m);
-        for (int64_t k = std::max<int64_t>(mb, 1); k < me; ++k)
-          good &= pe_prefix(k - 1) < pe_prefix(k);
-        const int64_t b = std::min<int64_t>(static_cast<int64_t>(r) * nper, n),
-                      e = std::min<int64_t>(b + nper, n);
-        if (good && b < e) {
-          good = b == 0 || query(b - 1) <= query(b);
-          const uint128 q0 = query(b);
-          int64_t lo = 0, hi = m;  // first stored prefix >= q0
-          while (lo < hi) {
-            const int64_t mid = lo + (hi - lo) / 2;
-            if (pe_prefix(mid) < q0)
-              lo = mid + 1;
-            else
-              hi = mid;
-          }
-          int64_t j = lo;
-          uint128 prev = q0;
-          for (int64_t i = b; i < e && good; ++i) {
-            const uint128 q = query(i);
-            if (q < prev) {
-              good = false;
-              break;
-            }
-            prev = q;
-            while (j < m && pe_prefix(j) < q) ++j;
-            if (j == m || pe_prefix(j) != q) {
-              good = false;
-              break;
-            }
-            seeds[i] = MakeUint128(pes[j].seed().high(), pes[j].seed().low());
-            cbs[i] = pes[j].control_bit() ? 1 : 0;
-          }
-        }
-        ok[r] = good;
+        const int64_t mb = std::min<int64_t>(static_cast<int64_t>(r) * mper, m);
+        const int64_t nb = std::min<int64_t>(static_cast<int64_t>(r) * nper, n);
+        ok[r] = stored_order(mb, std::min<int64_t>(mb + mper, m)) &&
+                merge_range(nb, std::min<int64_t>(nb + nper, n));
       });
       for (int64_t r = 0; r < parts; ++r) merged &= ok[r];
     }
+#else
+    if (merged) {
+      const int parts = pool.ParallelRanges(
+          m, 8192, [&](int r, int64_t b, int64_t e) { ok[r] = stored_order(b, e); });
+      for (int r = 0; r < parts; ++r) merged &= ok[r];
+    }
+    if (merged && n > 0) {
+      const int parts = pool.ParallelRanges(
+          n, 4096, [&](int r, int64_t b, int64_t e) { ok[r] = merge_range(b, e); });
+      for (int r = 0; r < parts; ++r) merged &= ok[r];
+    }
+#endif
     if (!merged) {
       std::unordered_map<uint128, std::pair<uint128, bool>, U128Hash> prev;
       prev.reserve(m * 2);
