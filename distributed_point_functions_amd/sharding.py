@@ -1,13 +1,14 @@
 """Multi-GPU partitioning of the hot path.
 
-One process per GPU. The DPF domain and the PIR database both partition
+One process per GPU. The DPF domain (c1, c5), EvaluateAt batches (c2), the
+incremental prefix lists (c3) and the PIR database (c4) all partition
 without any data-path exchange; the only collective is the all-gather of the
 tiny PIR partials (RCCL has no XOR reduction) and, for additive shares in
 Z_2^k (k <= 64), an all-reduce SUM that is exact under wraparound.
 """
 from __future__ import annotations
 
-from typing import Callable, Tuple
+from typing import Callable, List, Sequence, Tuple
 
 RECORDS_PER_SELECTION_BLOCK = 128  # bit r of block r/128 selects record r
 
@@ -33,6 +34,46 @@ def pir_row_shard(num_records: int, world: int, rank: int) -> Tuple[int, int, in
     r_lo = min(num_records, b_lo * RECORDS_PER_SELECTION_BLOCK)
     r_hi = min(num_records, b_hi * RECORDS_PER_SELECTION_BLOCK)
     return r_lo, r_hi, b_lo, b_hi
+
+
+def point_range(num_points: int, world: int, rank: int) -> Tuple[int, int]:
+    """c2 (EvaluateAt batches): `rank`'s contiguous slice [lo, hi) of the
+    points (or of the keys of a batched call); results concatenate in order,
+    no collective."""
+    return block_range(num_points, world, rank)
+
+
+def prefix_owner_bounds(prefixes: Sequence[int], world: int) -> List[int]:
+    """c3 (incremental evaluation): owner boundaries, in prefix values, for
+    the first prefixed hierarchy level.  `prefixes` is that level's sorted
+    candidate list; rank r owns the values [bounds[r], bounds[r + 1]) — a
+    contiguous, balanced slice of the list (equal values stay together).
+    Every later level's prefix p belongs to the rank that owns its ancestor
+    p >> (log_domain(level) - log_domain(first level)), which holds that
+    ancestor's partial evaluations in its own EvaluationContext (cc:374-476),
+    so no rank ever needs another's context."""
+    n = len(prefixes)
+    if world <= 0:
+        raise ValueError("bad world")
+    if any(prefixes[i] > prefixes[i + 1] for i in range(n - 1)):
+        raise ValueError("prefixes must be sorted")
+    bounds = [0]
+    for r in range(1, world):
+        lo, _ = block_range(n, world, r)
+        bounds.append(max(bounds[-1], prefixes[lo] if lo < n else (prefixes[-1] + 1 if n else 0)))
+    bounds.append(None)  # open upper end
+    return bounds
+
+
+def owned_prefixes(prefixes: Sequence[int], bounds: Sequence[int], rank: int,
+                   shift: int = 0) -> List[int]:
+    """The prefixes of a level owned by `rank` under `bounds`
+    (prefix_owner_bounds), `shift` = log_domain(level) - log_domain(first
+    prefixed level).  For a sorted list the ranks' slices are contiguous and
+    in rank order, so the ranks' outputs concatenate to the single-process
+    output."""
+    lo, hi = bounds[rank], bounds[rank + 1]
+    return [p for p in prefixes if (p >> shift) >= lo and (hi is None or (p >> shift) < hi)]
 
 
 def allgather_xor(part, world: int, fold: Callable = None):

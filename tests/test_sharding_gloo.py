@@ -70,6 +70,33 @@ def _worker(rank, world, port, q):
         res["dpf"] = np.array_equal(torch.cat(out).numpy().view(np.uint64),
                                     full.reshape(-1))
 
+        # (4) c2: EvaluateAt points in contiguous per-rank slices, concatenated.
+        pts = [int.from_bytes(rng.bytes(2), "little") % (1 << 12) for _ in range(101)]
+        plo, phi = sharding.point_range(len(pts), world, rank)
+        got = [None] * world
+        dist.all_gather_object(got, d.evaluate_at(k0, 0, pts[plo:phi]))
+        res["c2"] = [v for g in got for v in g] == d.evaluate_at(k0, 0, pts)
+
+        # (5) c3: each rank keeps its own context for the prefixes whose
+        # first-level ancestor it owns; every level's outputs concatenate.
+        lv = [(ld, spec, 40 + ld) for ld in (8, 16, 24)]
+        dd = po.Dpf(lv)
+        kk, _ = dd.generate_keys(0xABCDE, [11, 22, 33], seeds=(5, 6))
+        mine_ctx, full_ctx = dd.create_evaluation_context(kk), dd.create_evaluation_context(kk)
+        dd.evaluate_until(0, [], mine_ctx)
+        dd.evaluate_until(0, [], full_ctx)
+        p1 = sorted(int(x) for x in rng.choice(256, 60, replace=False)) + [255]
+        bounds = sharding.prefix_owner_bounds(p1, world)
+        ok3 = True
+        prefixes = p1
+        for h, shift in ((1, 0), (2, 8)):
+            mine = sharding.owned_prefixes(prefixes, bounds, rank, shift)
+            got = [None] * world
+            dist.all_gather_object(got, dd.evaluate_until(h, mine, mine_ctx) if mine else [])
+            ok3 &= [v for g in got for v in g] == dd.evaluate_until(h, prefixes, full_ctx)
+            prefixes = sorted({(p << 8) | int(y) for p in prefixes for y in (3, 200)})
+        res["c3"] = ok3
+
         # (3) Additive Z_2^64 shares summed over ranks wrap exactly.
         vals = [(2 ** 64 - 3), 5] if rank == 0 else [7, 2 ** 63 + 1]
         sh = torch.tensor(np.array(vals, dtype=np.uint64).view(np.int64))
@@ -94,6 +121,30 @@ def test_block_range_and_row_shards_cover_exactly():
             assert all(a[1] == b[0] for a, b in zip(rows, rows[1:]))
 
 
+def test_prefix_owners_partition_every_level():
+    """c3 ownership: every prefix of every level has exactly one owner, the
+    owners' slices are contiguous and in rank order (outputs concatenate),
+    and equal first-level prefixes share an owner."""
+    import random
+    rng = random.Random(3)
+    for world in (1, 2, 3, 8):
+        p1 = sorted(rng.randrange(1 << 10) for _ in range(97))
+        bounds = sharding.prefix_owner_bounds(p1, world)
+        levels = [(p1, 0)]
+        p2 = sorted({(p << 6) | rng.randrange(64) for p in p1 for _ in range(3)})
+        levels.append((p2, 6))
+        levels.append((sorted({(p << 6) | 5 for p in p2}), 12))
+        for prefixes, shift in levels:
+            parts = [sharding.owned_prefixes(prefixes, bounds, r, shift) for r in range(world)]
+            assert [x for part in parts for x in part] == prefixes
+        owner = {}
+        for r in range(world):
+            for p in sharding.owned_prefixes(p1, bounds, r):
+                assert owner.setdefault(p, r) == r
+    with pytest.raises(ValueError):
+        sharding.prefix_owner_bounds([3, 1], 2)
+
+
 def test_world_size_2_gloo():
     world = 2
     ctx = mp.get_context("spawn")
@@ -114,4 +165,5 @@ def test_world_size_2_gloo():
                 p.kill()
     for rank in range(world):
         assert "error" not in results[rank], results[rank]
-        assert results[rank] == {"pir": True, "dpf": True, "additive": True}, results[rank]
+        assert results[rank] == {"pir": True, "dpf": True, "c2": True, "c3": True,
+                                 "additive": True}, results[rank]

@@ -5,7 +5,11 @@ correct with [leaf_begin, leaf_end) from sharding.block_range) and scan
 their 128-aligned PIR row shard (dpf_amd_inner_product over sharding.pir_
 row_shard, selection bits expanded on the device for that block range).
 The gathered slices equal the oracle's full-domain expansion and the folded
-partials equal the oracle's inner product over the whole database.
+partials equal the oracle's inner product over the whole database.  c2 and c3
+partition the same way through the product's EvaluateAt / EvaluateNext:
+contiguous point slices, and prefixes owned by the rank that owns their
+first-level ancestor (sharding.prefix_owner_bounds), each rank with its own
+EvaluationContext; every level's gathered outputs equal the oracle's.
 """
 import os
 import socket
@@ -101,8 +105,47 @@ def _worker(rank, world, port, q):
             torch.cuda.synchronize()
             shares.append(sharding.allgather_xor(part.cpu(), world, fold=_host_fold).numpy())
         res["pir"] = bytes(shares[0] ^ shares[1]) == records[idx].tobytes()
-        # each party's folded share also equals the oracle's share (selection
-        # bits of that key over the whole database)
+
+        # (3) c2: EvaluateAt points in contiguous per-rank slices (product
+        # EvaluateAt on the device), concatenated == the oracle on all points
+        spec64 = ("int", 64)
+        vt64 = V.from_spec(spec64)
+        d2 = DistributedPointFunction.create(DpfParameters(40, vt64, 48))
+        od2 = po.Dpf([(40, spec64, 48)])
+        a2, b2, s2 = 0x12345678AB, 99, (7, 8)
+        key2, _ = d2.generate_keys(a2, b2, seeds=s2)
+        okey2, _ = od2.generate_keys(a2, [b2], seeds=s2)
+        prng = np.random.default_rng(23)
+        pts = [int(x) for x in prng.integers(0, 1 << 40, 3001, dtype=np.int64)] + [a2]
+        plo, phi = sharding.point_range(len(pts), world, rank)
+        got = [None] * world
+        dist.all_gather_object(got, vt64.decode_flat(d2.evaluate_at(key2, 0, pts[plo:phi],
+                                                                    raw=True)))
+        res["c2"] = [v for g in got for v in g] == od2.evaluate_at(okey2, 0, pts)
+
+        # (4) c3: each rank's own context holds the partial evaluations of the
+        # prefixes whose first-level ancestor it owns (product EvaluateNext)
+        lv = [(ld, spec64, 40 + ld) for ld in (8, 16, 24)]
+        d3 = DistributedPointFunction.create_incremental(
+            [DpfParameters(ld, vt64, sec) for ld, _, sec in lv])
+        od3 = po.Dpf(lv)
+        k3, _ = d3.generate_keys_incremental(0xABCDE, [11, 22, 33], seeds=(5, 6))
+        ok3k, _ = od3.generate_keys(0xABCDE, [11, 22, 33], seeds=(5, 6))
+        ctx = d3.create_evaluation_context(k3)
+        octx = od3.create_evaluation_context(ok3k)
+        d3.evaluate_next([], ctx, raw=True)
+        od3.evaluate_until(0, [], octx)
+        prefixes = sorted(int(x) for x in prng.choice(256, 80, replace=False))
+        bounds = sharding.prefix_owner_bounds(prefixes, world)
+        ok3 = True
+        for h, shift in ((1, 0), (2, 8)):
+            mine = sharding.owned_prefixes(prefixes, bounds, rank, shift)
+            got = [None] * world
+            dist.all_gather_object(
+                got, vt64.decode_flat(d3.evaluate_next(mine, ctx, raw=True)) if mine else [])
+            ok3 &= [v for g in got for v in g] == od3.evaluate_until(h, prefixes, octx)
+            prefixes = sorted({(p << 8) | y for p in prefixes for y in (3, 200)})
+        res["c3"] = bool(ok3)
         _lib.lib()
         dist.destroy_process_group()
         q.put((rank, res))
@@ -131,4 +174,4 @@ def test_world_size_2_product_data_path(cuda):
                 p.kill()
     for rank in range(world):
         assert "error" not in results[rank], results[rank]
-        assert results[rank] == {"dpf": True, "pir": True}, results[rank]
+        assert results[rank] == {"dpf": True, "pir": True, "c2": True, "c3": True}, results[rank]
