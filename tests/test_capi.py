@@ -36,6 +36,16 @@ def test_library_exports_every_declared_symbol():
     assert set(declared_functions()) <= exported
 
 
+def test_integration_index_lists_every_declared_symbol():
+    """INTEGRATION.md's generated index (tools/abi_index.py --write) names
+    every function the header declares, so the binding guide cannot fall
+    behind the boundary."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    begin, end = doc.index("<!-- abi-index:begin -->"), doc.index("<!-- abi-index:end -->")
+    listed = set(re.findall(r"\| `(dpf_amd_\w+)` \|", doc[begin:end]))
+    assert set(declared_functions()) == listed, set(declared_functions()) ^ listed
+
+
 def test_version_and_error_plumbing():
     L = _lib.lib()
     assert L.dpf_amd_version().decode().startswith("dpf_amd")
