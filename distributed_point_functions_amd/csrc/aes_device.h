@@ -52,11 +52,43 @@ struct Lds {
   uint32_t laneoff;
 };
 
+// Table fill.  Row e of the table is 64 words: T0[e] x 32 | T1[e] x 32.
+// DPF_FILL_SCALAR (default): wave w of the block writes rows 16w.. in chunks
+// of 16, each chunk's 16 entries read by one scalar load (s_load_dwordx16
+// through the constant cache, the row index is wave-uniform), then one
+// ds_write_b32 per row (lane l -> word l: conflict-free).  The previous
+// loop read an entry per word with 64-lane vector loads, eight in flight,
+// so a block waited two L2 round trips before its first lookup.
+#ifndef DPF_FILL_SCALAR
+#define DPF_FILL_SCALAR 1
+#endif
+template <bool T4>
+__device__ __forceinline__ void FillRows(uint32_t* tab) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int W = blockDim.x >> 6;  // blockDim.x is a multiple of 64, at most 1024
+  for (int r0 = w * 16; r0 < 256; r0 += W * 16) {
+    uint32_t e[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) e[r] = c_te0.t[r0 + r];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t v = (lane & 32) ? ((e[r] << 8) | (e[r] >> 24)) : e[r];  // T1 = rotl8(T0)
+      tab[(r0 + r) * 64 + lane] = v;
+      if (T4) tab[kTabWords + (r0 + r) * 64 + lane] = (v << 16) | (v >> 16);  // T2 / T3
+    }
+  }
+}
+
 __device__ __forceinline__ void FillTables(uint32_t* tab) {
+#if DPF_FILL_SCALAR
+  FillRows<false>(tab);
+#else
   for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) {
     uint32_t v = c_te0.t[i >> 6];
     tab[i] = (i & 32) ? ((v << 8) | (v >> 24)) : v;  // T1 = rotl8(T0)
   }
+#endif
 }
 
 __device__ __forceinline__ Lds MakeLds(const uint32_t* tab) {
@@ -436,6 +468,9 @@ __device__ __forceinline__ void QuadWalkStep(uint32_t& x, uint32_t& t, uint32_t 
 constexpr int kTab4Words = 2 * kTabWords;  // 128 KiB
 
 __device__ __forceinline__ void FillTables4(uint32_t* tab) {
+#if DPF_FILL_SCALAR
+  FillRows<true>(tab);
+#else
   for (int i = threadIdx.x; i < kTab4Words; i += blockDim.x) {
     const int j = i & (kTabWords - 1);
     uint32_t v = c_te0.t[j >> 6];
@@ -443,6 +478,7 @@ __device__ __forceinline__ void FillTables4(uint32_t* tab) {
     if (i >= kTabWords) v = (v << 16) | (v >> 16);  // T2 / T3 = rotl16(T0 / T1)
     tab[i] = v;
   }
+#endif
 }
 
 struct Lds4 {

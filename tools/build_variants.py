@@ -3,6 +3,7 @@ distributed_point_functions_amd/_native/var_<name>/libdpf_amd.so (select one
 at run time with DPF_AMD_LIB=<path>).  The other objects are the main build's.
 
     python tools/build_variants.py k_expand_c5.hip name1:DEF=1,DEF2=3 name2:...
+    python tools/build_variants.py all name:DEF=1     # every .hip TU
 """
 import concurrent.futures
 import os
@@ -24,10 +25,16 @@ def main():
         name, _, defs = spec.partition(":")
         d = os.path.join(B.OUT_DIR, "var_" + name)
         os.makedirs(d, exist_ok=True)
-        obj = B._compile(os.path.join(B.CSRC, tu), True, d, [x for x in defs.split(",") if x])
+        dl = [x for x in defs.split(",") if x]
+        if tu == "all":  # every device translation unit with the defines
+            mine = [B._compile(src, True, d, dl) for src in B._sources() if src.endswith(".hip")]
+            rest = [o for o in objs if not o.endswith(".hip.o")]
+            parts = mine + rest
+        else:
+            parts = [B._compile(os.path.join(B.CSRC, tu), True, d, dl)] + others
         lib = os.path.join(d, "libdpf_amd.so")
-        subprocess.check_call(["hipcc", "--offload-arch=" + B.ARCH, "-shared", "-fPIC", "-o", lib,
-                               obj] + others + ["-lpthread"])
+        subprocess.check_call(["hipcc", "--offload-arch=" + B.ARCH, "-shared", "-fPIC", "-o", lib] +
+                              parts + ["-lpthread"])
         return lib
 
     with concurrent.futures.ThreadPoolExecutor(8) as ex:
