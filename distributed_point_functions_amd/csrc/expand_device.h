@@ -459,43 +459,18 @@ extern "C" __attribute__((visibility("default"))) int dpf_amd_debug_coop_trace(v
 static_assert(kCoopBlock == 1024, "the BFS levels assume 1024 threads (64 -> 1024 nodes)");
 constexpr int kCoopLog = 10;  // log2 nodes after the BFS
 
-// T4 (launches of at most one block per CU): the block keeps four tables
-// (128 KiB, aes_device.h FillTables4), and the quad walk and the quad BFS
-// levels run AesQuadRk's four-table round with the moves after the lookups
-// (§3.3); the lane phases use the lower 64 KiB, the usual two tables.
-#ifndef DPF_COOP_T4_MAX_BLOCKS
-#define DPF_COOP_T4_MAX_BLOCKS 256
-#endif
-template <int E, class Em, bool kBatched, bool T4 = false>
+template <int E, class Em, bool kBatched>
 __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(ExpandArgs a,
                                                                           VtDev vt) {
-  __shared__ uint32_t tab[T4 ? kTab4Words : kTabWords];
+  __shared__ uint32_t tab[kTabWords];
   __shared__ uint4 nodes[kCoopBlock / 2];
   constexpr int BN = Em::kBN;
   constexpr int K = kCoopLog + E;  // log2 tree leaves per block
   DPF_COOP_MARK(0);
-  if constexpr (T4)
-    FillTables4(tab);
-  else
-    FillTables(tab);
+  FillTables(tab);
   __syncthreads();
   DPF_COOP_MARK(1);
   const Lds L = MakeLds(tab);
-  // the quad steps' tables: four (T4) or the two of L
-  using QL = std::conditional_t<T4, Lds4, Lds>;
-  QL LQ;
-  if constexpr (T4)
-    LQ = MakeLds4(tab);
-  else
-    LQ = L;
-  auto quad_step = [&](uint32_t& x, uint32_t& t, uint32_t bit, uint32_t cw_word, uint32_t cl,
-                       uint32_t cr, int c, const QuadKey& kl, const QuadRk& klr,
-                       const QuadDiff& kd) {
-    if constexpr (T4)
-      QuadWalkStepRk<true>(x, t, bit, cw_word, cl, cr, c, klr, kd, LQ);
-    else
-      QuadWalkStep(x, t, bit, cw_word, cl, cr, c, kl, kd, L);
-  };
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
@@ -514,7 +489,6 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
     const int c = lane & 3;
     const int q = wave * 16 + (lane >> 2);
     const QuadKey kl = MakeQuadKey<0>(c);
-    const QuadRk klr = MakeQuadRk<0>(c);
     const QuadDiff kd = MakeQuadDiff(c);
     const uint32_t* cw_words = reinterpret_cast<const uint32_t*>(a.cw_seed);
     uint32_t x = reinterpret_cast<const uint32_t*>(a.root_seeds)[root * 4 + c];
@@ -523,13 +497,13 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
     for (int i = 0; i < s; ++i) {
       const uint32_t bit = (uint32_t)(path >> (s - 1 - i)) & 1u;  // block-uniform
       const int64_t ci = cw0 + i;
-      quad_step(x, t, bit, cw_words[ci * 4 + c], a.ccl[ci], a.ccr[ci], c, kl, klr, kd);
+      QuadWalkStep(x, t, bit, cw_words[ci * 4 + c], a.ccl[ci], a.ccr[ci], c, kl, kd, L);
     }
 #pragma unroll 1
     for (int i = 0; i < 6; ++i) {
       const uint32_t bit = ((uint32_t)q >> (5 - i)) & 1u;
       const int64_t ci = cw0 + s + i;
-      quad_step(x, t, bit, cw_words[ci * 4 + c], a.ccl[ci], a.ccr[ci], c, kl, klr, kd);
+      QuadWalkStep(x, t, bit, cw_words[ci * 4 + c], a.ccl[ci], a.ccr[ci], c, kl, kd, L);
     }
     reinterpret_cast<uint32_t*>(nodes)[q * 4 + c] = c == 0 ? (x | t) : x;
   }
@@ -546,7 +520,6 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
     const int c = lane & 3;
     const int qd = tid >> 2;
     const QuadKey kl = MakeQuadKey<0>(c);
-    const QuadRk klr = MakeQuadRk<0>(c);
     const QuadDiff kd = MakeQuadDiff(c);
     const uint32_t* cw_words = reinterpret_cast<const uint32_t*>(a.cw_seed);
     uint32_t* nw = reinterpret_cast<uint32_t*>(nodes);
@@ -559,8 +532,8 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
         tq = QuadPerm<kQuadBcast<0>>(w) & 1u;
         xq = c == 0 ? (w & ~1u) : w;
         const int64_t ci = cw0 + s + 6 + j;
-        quad_step(xq, tq, (uint32_t)qd & 1u, cw_words[ci * 4 + c], a.ccl[ci], a.ccr[ci], c, kl,
-                  klr, kd);
+        QuadWalkStep(xq, tq, (uint32_t)qd & 1u, cw_words[ci * 4 + c], a.ccl[ci], a.ccr[ci], c,
+                     kl, kd, L);
       }
       __syncthreads();  // every parent of this level has been read
       if (active) nw[qd * 4 + c] = c == 0 ? (xq | tq) : xq;
@@ -650,12 +623,8 @@ int LaunchExpandCoop(hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
   }
   if (blocks < 1 || blocks > INT32_MAX)
     return SetError(DPF_AMD_INVALID_ARGUMENT, "expansion grid out of range");
-  if (blocks <= DPF_COOP_T4_MAX_BLOCKS)
-    hipLaunchKernelGGL((KExpandCoop<E, Em, false, true>), dim3((unsigned)blocks),
-                       dim3(kCoopBlock), 0, st, a, vt);
-  else
-    hipLaunchKernelGGL((KExpandCoop<E, Em, false>), dim3((unsigned)blocks), dim3(kCoopBlock), 0,
-                       st, a, vt);
+  hipLaunchKernelGGL((KExpandCoop<E, Em, false>), dim3((unsigned)blocks), dim3(kCoopBlock), 0, st,
+                     a, vt);
   return LaunchCheck("expand kernel launch");
 }
 
