@@ -316,9 +316,6 @@ __device__ __forceinline__ void Dfs(const ExpandCtx& E, LeafStage& S, const uint
 // Batched keys (kBatched, ExpandArgs::batched): lane i's chunk id maps to
 // key id / (chunk_end - chunk_begin) with that key's root, correction words,
 // value correction and party; leaf ranges and outputs are per key.
-#ifndef DPF_QUAD_UWALK
-#define DPF_QUAD_UWALK 1
-#endif
 template <int D, class Em, bool kBatched = false>
 __global__ __launch_bounds__(kBlockOf<Em>, kWavesOf<Em>) void KExpand(ExpandArgs a, VtDev vt) {
   __shared__ uint32_t tab[kTabWords];
@@ -342,40 +339,7 @@ __global__ __launch_bounds__(kBlockOf<Em>, kWavesOf<Em>) void KExpand(ExpandArgs
     uint4 s = a.root_seeds[root];
     uint32_t x[4] = {s.x, s.y, s.z, s.w};
     uint32_t t = a.root_cb[root];
-    int i0 = 0;
-#if DPF_QUAD_UWALK
-    // Walk levels whose path bit is the same for the whole wave, from a root
-    // the whole wave shares, compute the same seed in every lane: lane 0
-    // alone computes it (its table reads occupy the LDS for one lane, not
-    // 64) and the result is broadcast through SGPRs.  c5: the upper 18 of
-    // 24 walk levels, ~1.9 % of the kernel's lookup instructions.
-    if (!kBatched && __ballot(root != __builtin_amdgcn_readfirstlane(root)) == 0) {
-      const int lane = threadIdx.x & 63;
-      int n = 0;
-      while (n < a.walk) {
-        const uint32_t bit = (uint32_t)(path >> (a.walk - 1 - n)) & 1u;
-        if (__ballot(bit) != 0 && __ballot(bit ^ 1u) != 0) break;
-        ++n;
-      }
-      n = __builtin_amdgcn_readfirstlane(n);
-      if (n > 0) {
-        if (lane == 0) {
-#pragma unroll 1
-          for (int i = 0; i < n; ++i) {
-            const uint32_t ubit = __builtin_amdgcn_readfirstlane(
-                (uint32_t)(path >> (a.walk - 1 - i)) & 1u);
-            WalkStep(x, t, ubit, LoadCw(a.cw_seed, a.ccl, a.ccr, cw0 + i),
-                     DpfSelect{{}, ubit != 0}, L);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) x[k] = __builtin_amdgcn_readlane(x[k], 0);
-        t = __builtin_amdgcn_readlane(t, 0);
-        i0 = n;
-      }
-    }
-#endif
-    for (int i = i0; i < a.walk; ++i) {
+    for (int i = 0; i < a.walk; ++i) {
       const uint32_t bit = (uint32_t)(path >> (a.walk - 1 - i)) & 1u;
       const Cw cw = LoadCw(a.cw_seed, a.ccl, a.ccr, cw0 + i);
       // The upper path bits are shared by the whole wave: one AES with the
