@@ -312,6 +312,24 @@ def bench_in_process(args):
     return dict(wall=wall, leaves=total, L=dpf.hierarchy_to_tree(0), pir=pir)
 
 
+def m4_lds_roofline(db_bytes, q, ms, clock_ghz=2.4):
+    """LDS floor of one KPirScanM4 pass over `db_bytes` for q <= 64 queries:
+    (15 x 256 B / 128 B/clk + q x 256 B / 256 B/clk) per 4 records of 256 B,
+    at the 2.4 GHz peak clock and at the clock the profile of this build
+    measured under the kernel."""
+    kib = db_bytes / 1024
+    cycles_per_kib = 15 * 2 + q
+
+    def floor(ghz):
+        return kib * cycles_per_kib / (256 * ghz * 1e9) * 1e3
+    out = {"bound": "lds", "cycles_per_kib": cycles_per_kib, "clock_ghz": clock_ghz,
+           "floor_ms": floor(clock_ghz), "frac": floor(clock_ghz) / ms}
+    clk = clock_view(traffic_from_profiles(SCAN_M4_KERNEL_RE)[2])
+    if clk:
+        out["measured"] = dict(clk, frac_at_measured_clock=floor(clk["clock_ghz"]) / ms)
+    return out
+
+
 def library_sha256():
     import hashlib
     with open(_lib.LIB_PATH, "rb") as f:
@@ -355,6 +373,7 @@ def traffic_from_profiles(kernel_re):
 # the ones that identify the launch are matched loosely.
 EXPAND_C5_KERNEL_RE = r"KExpand<8, dpf_amd::EmitU32ModN64(, [^>]*)?>"
 SCAN_Q1_KERNEL_RE = r"KPirScanG<1, 4(, [^>]*)?>"
+SCAN_M4_KERNEL_RE = r"KPirScanM4<1>"
 
 
 def clock_view(entry):
@@ -662,6 +681,12 @@ def main():
                     "queries": pir["mq"], "ms_per_batch": pir["mq_ms"],
                     "query_GBps": pir["mq"] * pir["db_bytes"] / (pir["mq_ms"] / 1e3) / 1e9,
                     "db_GBps": pir["db_bytes"] / (pir["mq_ms"] / 1e3) / 1e9,
+                    # The Four-Russians scan is bound by its LDS work, not
+                    # HBM: per KiB of records 15 row stores
+                    # (ds_write_addtid_b32, 128 B/clk) + Q/4 row reads of
+                    # 256 B (ds_read_b128, 256 B/clk) = 94 LDS cycles at Q = 64.
+                    "lds_roofline": m4_lds_roofline(pir["per_gpu_bytes"], pir["mq"],
+                                                    pir["mq_ms"]),
                     "kernel": "KPirScanM4<1>+KXorFold (scan only, no selection DPF)"},
             }
             if pir.get("hr"):
