@@ -206,3 +206,11 @@ int PirScanM4Queries(int rem);
 int LaunchPirScanM4(int nq, int parts, int slices, hipStream_t st, const ScanArgs& a);
 
 }  // namespace dpf_amd
+
+// The T-table fill (aes_device.h FillRows) gives each wave whole table rows:
+// every block that fills tables has a multiple of 64 threads, at most 1024
+// (the run-time block sizes, WalkBlock and the quad launch, round to 64).
+static_assert(dpf_amd::kExpandBlock % 64 == 0 && dpf_amd::kExpandBlock <= 1024,
+              "expansion blocks must be whole waves");
+static_assert(dpf_amd::kPointsBlock % 64 == 0 && dpf_amd::kPointsBlock <= 1024,
+              "walk blocks must be whole waves");
