@@ -636,8 +636,12 @@ def main():
                          "achieved": lookups_s / 1e12,
                          "peak": LDS_PEAK_LOOKUPS / 1e12, "unit": "T lookups/s",
                          "frac": lookups_s / LDS_PEAK_LOOKUPS,
-                         "traffic": expand_traffic[0],
-                         "traffic_unit": "HBM bytes per launch (rocprofv3 PMC of this build)",
+                         # the profile is of the N = 1 launch (all 2^32 leaves);
+                         # a rank's launch expands 1/N of them
+                         "traffic": (expand_traffic[0] / world
+                                     if expand_traffic[0] is not None else None),
+                         "traffic_unit": "HBM bytes per launch (rocprofv3 PMC of this build%s)" %
+                                         (", N = 1 profile / %d ranks" % world if world > 1 else ""),
                          "traffic_error": expand_traffic[3],
                          "traffic_profile": expand_traffic[1],
                          "algorithmic_bytes": leaves // world * 16,
@@ -673,7 +677,9 @@ def main():
                 "scaling": "strong",
                 "roofline": {"bound": "hbm", "achieved": scan_gbs, "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": scan_gbs / HBM_PEAK_GBS,
-                             "traffic": scan_traffic[0], "traffic_profile": scan_traffic[1],
+                             "traffic": (scan_traffic[0] / world
+                                         if scan_traffic[0] is not None else None),
+                             "traffic_profile": scan_traffic[1],
                              "traffic_error": scan_traffic[3],
                              "algorithmic_bytes": pir["per_gpu_bytes"],
                              "kernel": "KPirScanG<1,4>+KXorFold", "kernel_ms": pir["scan_ms"]},
