@@ -100,27 +100,33 @@ class ValueType:
         return np.dtype({"names": names, "formats": formats, "offsets": offsets,
                          "itemsize": self.size})
 
-    def decode(self, arr: np.ndarray) -> list:
-        """Host-layout array -> list of Python values."""
+    def _columns(self, arr: np.ndarray) -> List[list]:
+        """One list of Python ints per scalar (ndarray.tolist converts in C;
+        128-bit scalars are (lo, hi) uint64 pairs)."""
         cols = []
         for i, s in enumerate(self.scalars()):
             c = arr["f%d" % i]
             if s.bits == 128:
-                cols.append([int(lo) | (int(hi) << 64) for lo, hi in c])
+                lo, hi = c[..., 0].tolist(), c[..., 1].tolist()
+                cols.append([a | (b << 64) for a, b in zip(lo, hi)])
             else:
-                cols.append([int(x) for x in c])
-        return [self.unflatten(iter(vals)) for vals in zip(*cols)] if cols else []
+                cols.append(c.tolist())
+        return cols
+
+    def decode(self, arr: np.ndarray) -> list:
+        """Host-layout array -> list of Python values."""
+        cols = self._columns(arr)
+        if not cols:
+            return []
+        if len(cols) == 1 and not isinstance(self, Tuple):
+            return cols[0]  # a plain scalar type: the values themselves
+        if isinstance(self, Tuple) and not any(isinstance(e, Tuple) for e in self.elements):
+            return list(zip(*cols))  # a flat tuple: one Python tuple per element
+        return [self.unflatten(iter(vals)) for vals in zip(*cols)]
 
     def decode_flat(self, arr: np.ndarray) -> List[List[int]]:
         """Host-layout array -> list of flattened scalar lists."""
-        cols = []
-        for i, s in enumerate(self.scalars()):
-            c = arr["f%d" % i]
-            if s.bits == 128:
-                cols.append([int(lo) | (int(hi) << 64) for lo, hi in c])
-            else:
-                cols.append([int(x) for x in c])
-        return [list(v) for v in zip(*cols)]
+        return [list(v) for v in zip(*self._columns(arr))]
 
     def descriptor(self, blocks_needed: int) -> "_lib.ValueTypeDesc":
         """dpf_amd_value_type for Tier-1 calls (blocks_needed from BitsNeeded)."""
@@ -326,6 +332,14 @@ def u128_words(values) -> np.ndarray:
         if values.dtype != np.uint64 or values.ndim != 2 or values.shape[1] != 2:
             raise ValueError("128-bit arrays must be (n, 2) uint64 {lo, hi} rows")
         return np.ascontiguousarray(values).reshape(-1)
+    try:  # all values below 2^64 (the common case): converted in C
+        lo = np.array(values, dtype=np.uint64).reshape(-1)
+        if lo.shape[0] == len(values):
+            out = np.zeros((len(values), 2), dtype=np.uint64)
+            out[:, 0] = lo
+            return out.reshape(-1)
+    except (OverflowError, TypeError, ValueError):
+        pass
     lo = np.fromiter((int(v) & MASK64 for v in values), dtype=np.uint64, count=len(values))
     hi = np.fromiter(((int(v) >> 64) & MASK64 for v in values), dtype=np.uint64,
                      count=len(values))
