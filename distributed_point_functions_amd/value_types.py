@@ -332,14 +332,25 @@ def u128_words(values) -> np.ndarray:
         if values.dtype != np.uint64 or values.ndim != 2 or values.shape[1] != 2:
             raise ValueError("128-bit arrays must be (n, 2) uint64 {lo, hi} rows")
         return np.ascontiguousarray(values).reshape(-1)
-    try:  # all values below 2^64 (the common case): converted in C
+    def small():  # all values below 2^64: converted in C
         lo = np.array(values, dtype=np.uint64).reshape(-1)
-        if lo.shape[0] == len(values):
-            out = np.zeros((len(values), 2), dtype=np.uint64)
-            out[:, 0] = lo
-            return out.reshape(-1)
-    except (OverflowError, TypeError, ValueError):
-        pass
+        if lo.shape[0] != len(values):
+            raise ValueError
+        out = np.zeros((len(values), 2), dtype=np.uint64)
+        out[:, 0] = lo
+        return out.reshape(-1)
+
+    def wide():  # Python ints in [0, 2^128): their little-endian bytes are the words
+        return np.frombuffer(b"".join(v.to_bytes(16, "little") for v in values),
+                             dtype=np.uint64).copy()
+    # try first the form the first value suggests; either is exact or raises
+    first = values[0] if len(values) else 0
+    order = (wide, small) if isinstance(first, int) and first >> 64 else (small, wide)
+    for f in order:
+        try:
+            return f()
+        except (OverflowError, AttributeError, TypeError, ValueError):
+            pass
     lo = np.fromiter((int(v) & MASK64 for v in values), dtype=np.uint64, count=len(values))
     hi = np.fromiter(((int(v) >> 64) & MASK64 for v in values), dtype=np.uint64,
                      count=len(values))
