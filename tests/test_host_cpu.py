@@ -285,3 +285,55 @@ def test_dcf_value_proto_needs_registration():
     assert e.value.code == 9
     d.generate_keys(17, (1, 2))  # templated: registers
     d.generate_keys(17, vt.value_proto((1, 2)))
+
+
+@pytest.mark.parametrize("spec", [("int", 8), ("int", 64), ("int", 128), ("xor", 128),
+                                  ("intmodn", 64, 2 ** 64 - 59),
+                                  ("tuple", [("int", 32), ("intmodn", 64, 2 ** 64 - 59)]),
+                                  ("tuple", [("int", 16), ("tuple", [("int", 8), ("xor", 128)])])])
+def test_decode_matches_elementwise_conversion(spec):
+    """ValueType.decode / decode_flat (ndarray.tolist fast paths) equal the
+    element-by-element conversion they replace, for plain, flat-tuple and
+    nested-tuple types."""
+    import numpy as np
+    from distributed_point_functions_amd import value_types as V
+    vt = V.from_spec(spec)
+    raw = np.frombuffer(np.random.default_rng(3).bytes(257 * vt.numpy_dtype().itemsize),
+                        dtype=vt.numpy_dtype())
+    cols = []
+    for i, s in enumerate(vt.scalars()):
+        c = raw["f%d" % i]
+        cols.append([int(lo) | (int(hi) << 64) for lo, hi in c] if s.bits == 128
+                    else [int(x) for x in c])
+    assert vt.decode(raw) == [vt.unflatten(iter(v)) for v in zip(*cols)]
+    assert vt.decode_flat(raw) == [list(v) for v in zip(*cols)]
+
+
+def test_u128_words_every_input_form():
+    """128-bit packing: small ints, wide ints, mixed, negative (two's
+    complement, as the reference's absl::uint128 conversion), numpy scalars,
+    and (n, 2) uint64 arrays passed through."""
+    import numpy as np
+    from distributed_point_functions_amd.value_types import MASK64, u128_words
+
+    def ref(values):
+        return np.array([[int(v) & MASK64, (int(v) >> 64) & MASK64] for v in values],
+                        dtype=np.uint64).reshape(-1)
+    rng = np.random.default_rng(4)
+    cases = [[int(x) for x in rng.integers(0, 2 ** 63, 100)],
+             [int.from_bytes(rng.bytes(16), "little") for _ in range(100)],
+             [5, 2 ** 100, 0, 2 ** 128 - 1], [2 ** 64, 1], [-1, 3], [np.uint64(9), 2 ** 70], []]
+    for values in cases:
+        assert np.array_equal(u128_words(values), ref(values)), values[:3]
+    arr = np.array([[1, 2], [3, 4]], dtype=np.uint64)
+    assert np.array_equal(u128_words(arr), arr.reshape(-1))
+
+
+def test_bench_lds_roofline_of_the_many_query_scan():
+    """bench.py's floor for the 64-query Four-Russians pass: 15 row stores
+    at 128 B/clk + 64 row reads at 256 B/clk per KiB = 94 LDS cycles."""
+    import bench
+    r = bench.m4_lds_roofline(1 << 34, 64, 4.0)
+    assert r["cycles_per_kib"] == 94
+    assert abs(r["floor_ms"] - (1 << 24) * 94 / (256 * 2.4e9) * 1e3) < 1e-9
+    assert abs(r["frac"] - r["floor_ms"] / 4.0) < 1e-12
