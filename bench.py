@@ -61,11 +61,64 @@ AES_PER_LEAF_C5 = 4.0          # 2(2^32-1) tree + 2 * 2^32 value AES per 2^32 le
 # last-round lookups — DESIGN.md §3.1).  Measured SQ_INSTS_LDS x 64 / leaf:
 # 615 = 601 + the root-to-subtree walk (24 AES per 256-leaf subtree).
 LDS_LOOKUPS_PER_LEAF_C5 = 601
+# I_AES: VALU lane-instructions per AES block of the c5
+# kernel, SQ_INSTS_VALU x 64 / (4 x 2^32) of profiles/r04g_pmc.json; the
+# bench line recomputes it from a PMC profile of the loaded build when one
+# is committed.
+I_AES_C5 = 307.2
 
 
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print("[bench]", *a, flush=True)
+
+
+def bench_backend():
+    return os.environ.get("DPF_AMD_BENCH_BACKEND", "nccl")
+
+
+def launch_decision(args, env, device_count):
+    """How `bench.py --gpus N` gets its N ranks, decided before any GPU call.
+
+    Returns ("run", None) when this process is the whole job or one rank of
+    an already launched one (WORLD_SIZE set), ("spawn", N) when it must start
+    N rank processes itself (--gpus N > 1 and no WORLD_SIZE), or ("error",
+    message) when the request cannot be honoured: a world size that is not
+    --gpus, or more RCCL ranks than visible GPUs.  --in-process and
+    --experiments drive their devices from this one process."""
+    if args.in_process or args.experiments:
+        return "run", None
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != args.gpus:
+            return "error", ("launched with WORLD_SIZE=%s but --gpus %d: the line would not "
+                             "describe the job" % (world, args.gpus))
+        return "run", None
+    if args.gpus <= 1:
+        return "run", None
+    if env.get("DPF_AMD_BENCH_BACKEND", "nccl") == "nccl" and args.gpus > device_count:
+        return "error", ("--gpus %d with RCCL needs %d GPUs, %d visible (set "
+                         "DPF_AMD_BENCH_BACKEND=gloo to rehearse N ranks on fewer GPUs)"
+                         % (args.gpus, args.gpus, device_count))
+    return "spawn", args.gpus
+
+
+def spawn_ranks(n, argv):
+    """Start the N-rank job as a child (torch.distributed.run on 127.0.0.1,
+    one process per GPU) and return its exit code; rank 0 prints the line.
+    This process has not touched the GPU, and it does not exec."""
+    import socket
+    import subprocess
+    import sys
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % n, "--master-addr=127.0.0.1", "--master-port=%d" % port,
+           os.path.abspath(__file__)] + list(argv)
+    print("[bench] --gpus %d without WORLD_SIZE: starting %d rank processes (%s)"
+          % (n, n, " ".join(cmd[1:5])), flush=True)
+    return subprocess.call(cmd)
 
 
 def setup():
@@ -76,7 +129,7 @@ def setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    backend = os.environ.get("DPF_AMD_BENCH_BACKEND", "nccl")
+    backend = bench_backend()
     if backend != "nccl":
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -85,7 +138,24 @@ def setup():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != world:
+            raise SystemExit("process group has %d ranks, WORLD_SIZE=%d"
+                             % (dist.get_world_size(), world))
     return world, rank, torch.device("cuda", local)
+
+
+def rank_devices(world, device):
+    """[(rank, device index, PCI bus id)] of every rank, gathered to all."""
+    props = torch.cuda.get_device_properties(device)
+    mine = (int(os.environ.get("RANK", "0")), device.index,
+            "%04x:%02x:%02x" % (getattr(props, "pci_domain_id", 0),
+                                getattr(props, "pci_bus_id", 0),
+                                getattr(props, "pci_device_id", 0)))
+    if world == 1:
+        return [mine]
+    out = [None] * world
+    dist.all_gather_object(out, mine)
+    return out
 
 
 def barrier(world):
@@ -395,6 +465,20 @@ def clock_view(entry):
     return out
 
 
+def valu_view(aes_s, entry):
+    """VALU lane-instructions per second of the c5 kernel against the issue
+    peak, with I_AES from the PMC entry of this build (its launch covers the
+    whole 2^32 domain: 4 x 2^32 AES) or the frozen round-4 figure."""
+    i_aes, src = I_AES_C5, "frozen: profiles/r04g_pmc.json"
+    c = (entry or {}).get("counters_per_launch", {})
+    if "SQ_INSTS_VALU" in c:
+        i_aes, src = c["SQ_INSTS_VALU"] * 64 / (AES_PER_LEAF_C5 * 2 ** 32), "PMC of this build"
+    achieved = aes_s * i_aes
+    return {"i_aes": i_aes, "i_aes_source": src, "achieved": achieved / 1e12,
+            "peak": VALU_PEAK_TOPS, "unit": "T lane-instructions/s",
+            "frac": achieved / (VALU_PEAK_TOPS * 1e12)}
+
+
 def _cpu_worker(job):
     """One CPU-baseline process: oracle expansion of 2^20-leaf subtrees
     first, first + stride, ... of the c5 key for `seconds`."""
@@ -570,7 +654,7 @@ def main_experiments(args):
                       "all_correct": all(r.get("correct") for r in rows)}), flush=True)
 
 
-def main():
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -593,7 +677,15 @@ def main():
     ap.add_argument("--in-process", action="store_true",
                     help="drive all --gpus GPUs from this one process through the library's "
                          "multi-GPU API (ExpandLeavesOnDevices, a sharded DenseDpfPirDatabase)")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+    # torch.cuda.device_count() does not initialise the GPU on this image
+    how, what = launch_decision(args, os.environ, torch.cuda.device_count())
+    if how == "error":
+        print("[bench] error: " + what, flush=True)
+        return 2
+    if how == "spawn":
+        import sys
+        return spawn_ranks(what, sys.argv[1:] if argv is None else argv)
     if args.experiments:
         return main_experiments(args)
     if args.in_process:
@@ -601,11 +693,15 @@ def main():
             _lib.lib().dpf_amd_set_force_peer_copies(1)
         return main_in_process(args)
     world, rank, device = setup()
+    ranks = rank_devices(world, device)
     r = bench_dpf(args, world, rank, device)
     pir = None if args.skip_pir else bench_pir(args, world, rank, device)
     cpu = None
-    if rank == 0 and world == 1 and not args.skip_cpu_baseline:
+    # rank 0 times the host CPU after the GPU legs, the other ranks wait
+    if rank == 0 and not args.skip_cpu_baseline:
         cpu = cpu_baseline(args)
+    if world > 1:
+        dist.barrier()
     if rank == 0:
         leaves = r["leaves"]
         ms = 1000 * r["wall"] / args.steps
@@ -628,6 +724,9 @@ def main():
                        "leaves_per_step": leaves, "tree_levels": r["L"],
                        "parallelism": "one key's 2^%d domain subtree-sharded over %d GPU(s)" %
                                       (args.log_domain, world)},
+            "world_size": world, "backend": bench_backend() if world > 1 else None,
+            # (rank, device index, PCI bus id) of every rank
+            "rank_devices": ranks,
             # The T-table AES is bound by LDS lookup issue (ds_read_b32: 32
             # lane-lookups/clk/CU, conflict-free by construction): achieved =
             # leaves per launch x 601 lookups / kernel time (the subtree walk's
@@ -654,6 +753,10 @@ def main():
                          "measured": (dict(clk, frac_at_measured_clock=(
                              lookups_s / (LDS_PEAK_LOOKUPS * clk["clock_ghz"] / 2.4)))
                              if clk else None)},
+            # SURVEY.md §8d's integer-VALU fraction: AES/s x I_AES / the
+            # VALU issue peak (256 CU x 4 SIMD x 32 lanes x 2.4 GHz; the
+            # 64-lane figure of BASELINE.md:56 undercounts CDNA4's SIMDs by 2)
+            "valu": valu_view(aes_s, expand_traffic[2]),
             # Not a roofline: the implementation-independent reference point
             # of SURVEY.md §8d — AES/s priced at the 757.5 two-input gate ops
             # a bitsliced AES-128 needs per block, against the VALU issue
@@ -733,13 +836,20 @@ def main_in_process(args):
         "roofline": {"bound": "lds", "achieved": lookups_s / 1e12,
                      "peak": LDS_PEAK_LOOKUPS / 1e12, "unit": "T lookups/s",
                      "frac": lookups_s / LDS_PEAK_LOOKUPS,
-                     "traffic": expand_traffic[0], "traffic_profile": expand_traffic[1],
+                     # the profile is of the N = 1 launch (all leaves); each
+                     # GPU's slices expand 1/N of them
+                     "traffic": (expand_traffic[0] / args.gpus
+                                 if expand_traffic[0] is not None else None),
+                     "traffic_unit": "HBM bytes per GPU per step (rocprofv3 PMC of this build%s)"
+                                     % (", N = 1 profile / %d GPUs" % args.gpus
+                                        if args.gpus > 1 else ""),
+                     "traffic_profile": expand_traffic[1],
                      "traffic_error": expand_traffic[3],
                      "algorithmic_bytes": int(per_gpu_leaves) * 16,
                      "kernel": "KExpand<8,EmitU32ModN64>", "kernel_ms": ms,
                      "kernel_ms_is": "step wall time of ExpandLeavesOnDevices",
                      "lookups_per_leaf": LDS_LOOKUPS_PER_LEAF_C5},
-        "cpu_baseline": None,
+        "cpu_baseline": None if args.skip_cpu_baseline else cpu_baseline(args),
     }
     if r["pir"]:
         p = r["pir"]
@@ -766,4 +876,4 @@ def main_in_process(args):
 
 
 if __name__ == "__main__":
-    main()
+    raise SystemExit(main())

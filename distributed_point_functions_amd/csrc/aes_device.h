@@ -66,7 +66,9 @@ template <bool T4>
 __device__ __forceinline__ void FillRows(uint32_t* tab) {
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int W = blockDim.x >> 6;  // blockDim.x is a multiple of 64, at most 1024
+  // blockDim.x is a multiple of 64, at most 1024; a block below one wave
+  // would otherwise never advance r0
+  const int W = max(1, static_cast<int>(blockDim.x >> 6));
   for (int r0 = w * 16; r0 < 256; r0 += W * 16) {
     uint32_t e[16];
 #pragma unroll

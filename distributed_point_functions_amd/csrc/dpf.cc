@@ -987,7 +987,11 @@ Status ValidateDpfKey(const DpfState& st, const DpfKey& key) {
   return OkStatus();
 }
 
-Status ValidateEvaluationContext(const DpfState& st, const EvaluationContext& ctx) {
+// `for_evaluate_at`: EvaluateAt may target any level of a context, so the
+// "fully evaluated" check is skipped; the stored levels must still index the
+// hierarchy (a parsed context is untrusted bytes).
+Status ValidateEvaluationContext(const DpfState& st, const EvaluationContext& ctx,
+                                 bool for_evaluate_at = false) {
   if (ctx.parameters_size() != static_cast<int>(st.parameters.size()))
     return InvalidArgumentError("Number of parameters in `ctx` doesn't match");
   for (int i = 0; i < ctx.parameters_size(); ++i) {
@@ -997,8 +1001,13 @@ Status ValidateEvaluationContext(const DpfState& st, const EvaluationContext& ct
   }
   if (!ctx.has_key()) return InvalidArgumentError("ctx.key must be present");
   DPF_RETURN_IF_ERROR(ValidateDpfKey(st, ctx.key()));
-  if (ctx.previous_hierarchy_level() >= ctx.parameters_size() - 1)
+  const int num_levels = ctx.parameters_size();
+  if (!for_evaluate_at && ctx.previous_hierarchy_level() >= num_levels - 1)
     return InvalidArgumentError("This context has already been fully evaluated");
+  if (ctx.previous_hierarchy_level() < -1 || ctx.previous_hierarchy_level() >= num_levels)
+    return InvalidArgumentError("ctx.previous_hierarchy_level out of range");
+  if (ctx.partial_evaluations_level() < 0 || ctx.partial_evaluations_level() >= num_levels)
+    return InvalidArgumentError("ctx.partial_evaluations_level out of range");
   if (!ctx.partial_evaluations().empty() &&
       ctx.partial_evaluations_level() > ctx.previous_hierarchy_level())
     return InvalidArgumentError(
@@ -1753,6 +1762,7 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
                                   "]` larger than the domain size at hierarchy level " +
                                   std::to_string(hierarchy_level));
   DPF_RETURN_IF_ERROR(ValidateDpfKey(st, key));
+  if (ctx != nullptr) DPF_RETURN_IF_ERROR(ValidateEvaluationContext(st, *ctx, true));
   if (n == 0) return OkStatus();
   const LevelMeta& m = st.levels[hierarchy_level];
   dpf_amd_value_type vt;

@@ -332,10 +332,15 @@ def u128_words(values) -> np.ndarray:
         if values.dtype != np.uint64 or values.ndim != 2 or values.shape[1] != 2:
             raise ValueError("128-bit arrays must be (n, 2) uint64 {lo, hi} rows")
         return np.ascontiguousarray(values).reshape(-1)
-    def small():  # all values below 2^64: converted in C
-        lo = np.array(values, dtype=np.uint64).reshape(-1)
-        if lo.shape[0] != len(values):
+    def small():  # all values in [0, 2^64): converted in C
+        arr = np.asarray(values)
+        if arr.dtype.kind not in "iu" or arr.ndim != 1 or arr.shape[0] != len(values):
             raise ValueError
+        if arr.dtype.kind == "i" and arr.min() < 0:
+            # a cast would wrap a negative (numpy) int to 64 bits; the exact
+            # path below extends it to 128 bits as absl::uint128 does
+            raise ValueError
+        lo = arr.astype(np.uint64)
         out = np.zeros((len(values), 2), dtype=np.uint64)
         out[:, 0] = lo
         return out.reshape(-1)

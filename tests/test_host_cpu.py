@@ -322,7 +322,9 @@ def test_u128_words_every_input_form():
     rng = np.random.default_rng(4)
     cases = [[int(x) for x in rng.integers(0, 2 ** 63, 100)],
              [int.from_bytes(rng.bytes(16), "little") for _ in range(100)],
-             [5, 2 ** 100, 0, 2 ** 128 - 1], [2 ** 64, 1], [-1, 3], [np.uint64(9), 2 ** 70], []]
+             [5, 2 ** 100, 0, 2 ** 128 - 1], [2 ** 64, 1], [-1, 3], [np.uint64(9), 2 ** 70], [],
+             [np.int64(-1)], [np.int64(-5), np.int64(7)], [np.int32(-2)], [2 ** 63, 1],
+             [np.uint64(2 ** 64 - 1)], [True, 0]]
     for values in cases:
         assert np.array_equal(u128_words(values), ref(values)), values[:3]
     arr = np.array([[1, 2], [3, 4]], dtype=np.uint64)
@@ -337,3 +339,69 @@ def test_bench_lds_roofline_of_the_many_query_scan():
     assert r["cycles_per_kib"] == 94
     assert abs(r["floor_ms"] - (1 << 24) * 94 / (256 * 2.4e9) * 1e3) < 1e-9
     assert abs(r["frac"] - r["floor_ms"] / 4.0) < 1e-12
+
+
+def test_bench_launch_decision():
+    """bench.py --gpus N: spawns its N ranks when nothing launched them, runs
+    as one rank when WORLD_SIZE matches, refuses a mismatched world size or
+    more RCCL ranks than GPUs; --in-process / --experiments stay one process."""
+    import argparse
+    import bench
+
+    def a(gpus, **kw):
+        return argparse.Namespace(gpus=gpus, in_process=kw.get("ip", False),
+                                  experiments=kw.get("ex", False))
+    assert bench.launch_decision(a(1), {}, 1) == ("run", None)
+    assert bench.launch_decision(a(8), {}, 8) == ("spawn", 8)
+    assert bench.launch_decision(a(8), {"WORLD_SIZE": "8"}, 8) == ("run", None)
+    assert bench.launch_decision(a(1), {"WORLD_SIZE": "1"}, 8) == ("run", None)
+    how, msg = bench.launch_decision(a(8), {"WORLD_SIZE": "1"}, 8)
+    assert how == "error" and "WORLD_SIZE=1" in msg
+    how, msg = bench.launch_decision(a(2), {}, 1)
+    assert how == "error" and "DPF_AMD_BENCH_BACKEND=gloo" in msg
+    assert bench.launch_decision(a(2), {"DPF_AMD_BENCH_BACKEND": "gloo"}, 1) == ("spawn", 2)
+    assert bench.launch_decision(a(4, ip=True), {}, 1) == ("run", None)
+    assert bench.launch_decision(a(4, ex=True), {}, 1) == ("run", None)
+
+
+def test_bench_spawns_ranks_without_torchrun():
+    """`bench.py --gpus 2` with no launcher starts torch.distributed.run as a
+    child with 2 ranks (on CPU the ranks stop at their first device call, so
+    only the launch and its exit status are checked)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DPF_AMD_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--steps", "1"], capture_output=True, text=True, env=env, timeout=300)
+    assert "starting 2 rank processes" in p.stdout
+    assert "--nproc-per-node=2" in p.stdout
+    assert p.returncode != 0  # no GPU here: the ranks fail, and the parent says so
+
+
+def test_evaluate_at_ctx_rejects_out_of_range_context_levels():
+    """A parsed (untrusted) EvaluationContext whose stored levels do not index
+    the hierarchy is INVALID_ARGUMENT before any host table lookup or device
+    work (EvaluateAt h:356-378 with ctx; the levels are fields 3 and 5 of
+    the proto, and a repeated scalar field's last value wins)."""
+    dpf = DistributedPointFunction.create_incremental(
+        [DpfParameters(5, V.UINT64), DpfParameters(10, V.UINT64)])
+    k0, _ = dpf.generate_keys_incremental(3, [1, 2], seeds=(11, 12))
+    data = dpf.create_evaluation_context(k0).serialize()
+    for field, v, what in ((5, 99, "partial_evaluations_level"),
+                           (5, -1, "partial_evaluations_level"),
+                           (5, 2, "partial_evaluations_level"),
+                           (3, 7, "previous_hierarchy_level"),
+                           (3, -5, "previous_hierarchy_level")):
+        ctx = dpf.parse_evaluation_context(data + wire.field_varint(field, v))
+        e = _err(lambda: dpf.evaluate_at_ctx(1, [3], ctx))
+        assert e.code == 3 and e.message == "ctx.%s out of range" % what, (field, v)
+        e = _err(lambda: dpf.evaluate_at_ctx(1, [], ctx))  # before the empty-points return
+        assert e.code == 3, (field, v)
+    # a context of other parameters
+    other = DistributedPointFunction.create_incremental(
+        [DpfParameters(6, V.UINT64), DpfParameters(10, V.UINT64)])
+    ctx = other.parse_evaluation_context(data)
+    e = _err(lambda: other.evaluate_at_ctx(1, [3], ctx))
+    assert e.code == 3

@@ -4,6 +4,11 @@ wall time; run with DPF_AMD_TRACE_HOST=1 for the library's phase times and
 under rocprofv3 --kernel-trace for the kernels.
 
     python tools/pir_hr_probe.py [--queries 1,8,64] [--reps 5] [--log-n 26]
+        [--devices 0,0,0,0,0,0,0,0] [--force-peer]
+
+--devices shards the rows over the listed devices (entries may repeat: N
+shards' code on fewer GPUs); --force-peer takes the cross-device copy
+branches between shards on one device.
 """
 import argparse
 import os
@@ -21,15 +26,21 @@ def main():
     ap.add_argument("--queries", default="1,8,64")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--log-n", type=int, default=26)
+    ap.add_argument("--devices", default="")
+    ap.add_argument("--force-peer", action="store_true")
     args = ap.parse_args()
     import torch
+    from distributed_point_functions_amd import _lib
     from distributed_point_functions_amd import pir as P
     from distributed_point_functions_amd import value_types as V
     from distributed_point_functions_amd.dpf import DistributedPointFunction, DpfParameters
     n, rec = 1 << args.log_n, 256
     dev = torch.device("cuda", 0)
     rows = torch.randint(0, 256, (n * rec,), dtype=torch.uint8, device=dev)
-    db = P.DenseDpfPirDatabase()
+    if args.force_peer:
+        _lib.lib().dpf_amd_set_force_peer_copies(1)
+    devs = [int(d) for d in args.devices.split(",")] if args.devices else None
+    db = P.DenseDpfPirDatabase(devs)
     db.insert_fixed_device(rows, n, rec).build()
     server = P.DenseDpfPirServer.create_plain(n, db)
     dpf = DistributedPointFunction.create(DpfParameters((n - 1).bit_length(), V.XorWrapper(128)))
@@ -44,7 +55,8 @@ def main():
             t0 = time.perf_counter()
             server.handle_request(req)
             ts.append(1e3 * (time.perf_counter() - t0))
-        print("Q=%d best %.3f ms mean %.3f ms" % (q, min(ts), sum(ts) / len(ts)), flush=True)
+        print("Q=%d shards=%d best %.3f ms mean %.3f ms" % (q, len(devs or [0]), min(ts),
+                                                          sum(ts) / len(ts)), flush=True)
 
 
 if __name__ == "__main__":
