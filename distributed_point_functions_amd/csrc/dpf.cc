@@ -2037,18 +2037,28 @@ Status DistributedPointFunction::ExpandLeavesOnDevice(const DpfKey& key, int64_t
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ThreadStream();
   const uint128 seed = MakeUint128(key.seed().high(), key.seed().low());
   const uint8_t cb = static_cast<uint8_t>(key.party() != 0);
-  CwArrays cw = KeyCws(key, 0, m.tree_level);
-  DeviceBuffer rs, rc, cws, ccl, ccr;
-  DPF_RETURN_IF_ERROR(rs.Upload(&seed, 16, s));
-  DPF_RETURN_IF_ERROR(rc.Upload(&cb, 1, s));
-  DPF_RETURN_IF_ERROR(cws.Upload(cw.seeds.data(), 16 * m.tree_level, s));
-  DPF_RETURN_IF_ERROR(ccl.Upload(cw.ccl.data(), m.tree_level, s));
-  DPF_RETURN_IF_ERROR(ccr.Upload(cw.ccr.data(), m.tree_level, s));
-  const int cepb = 1 << (m.log_domain - m.tree_level);
+  const int L = m.tree_level;
+  CwArrays cw = KeyCws(key, 0, L);
+  // the key's inputs in one pinned slot and one copy (a PIR request's
+  // selection expansion sits on the critical path in front of the scan)
+  using Part = UploadRing::HostPart;
+  const Part parts[5] = {{&seed, 16},
+                         {&cb, 1},
+                         {cw.seeds.data(), size_t(16) * L},
+                         {cw.ccl.data(), size_t(L)},
+                         {cw.ccr.data(), size_t(L)}};
+  size_t off[5];
+  const size_t bytes = UploadRing::PackedLayout(parts, 5, off);
+  DeviceBuffer in;
+  DPF_RETURN_IF_ERROR(in.Alloc(bytes, s));
+  char* d = in.as<char>();
+  DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 5, bytes, off, s));
+  const int cepb = 1 << (m.log_domain - L);
   return AbiStatus(dpf_amd_expand_and_correct(
-      1, rs.get(), rc.as<uint8_t>(), m.tree_level, cws.get(), ccl.as<uint8_t>(),
-      ccr.as<uint8_t>(), &vt, reinterpret_cast<const uint64_t*>(corr.data()), key.party(), cepb,
-      leaf_begin, leaf_end, out, s));
+      1, d + off[0], reinterpret_cast<const uint8_t*>(d + off[1]), L, d + off[2],
+      reinterpret_cast<const uint8_t*>(d + off[3]), reinterpret_cast<const uint8_t*>(d + off[4]),
+      &vt, reinterpret_cast<const uint64_t*>(corr.data()), key.party(), cepb, leaf_begin,
+      leaf_end, out, s));
 }
 
 

@@ -108,4 +108,22 @@ int PrefixRoots(int64_t n, const int32_t* idx, const uint8_t* low, int walk, int
                 const void* seeds, const uint8_t* cb, const void* cw_seed, const uint8_t* ccl,
                 const uint8_t* ccr, void* seeds_out, uint8_t* cb_out, void* stream);
 
+// Dense-PIR scan of one database piece, split from its fold so several
+// pieces on one device can share one workspace and one fold
+// (dpf_amd_inner_product = PlanScan + [slot memset] + ScanPiece + fold).
+// With `slots` every block XORs its partial atomically into one of
+// kScanSlots partials (the workspace must be zeroed first; pieces may share
+// the slots); otherwise block b writes partial b of `partials`.  The fold
+// then reads ScanFoldParts(plan) partials of num_queries x record_stride
+// bytes.  Device pointers, stream-ordered.
+struct ScanPlan {
+  int grid = 1;
+  bool slots = false;
+};
+ScanPlan PlanScan(int64_t num_records, int64_t record_stride, int num_queries);
+int ScanFoldParts(const ScanPlan& plan);
+int ScanPiece(const void* db, int64_t num_records, int64_t record_stride,
+              const void* selections, int64_t selection_blocks, int num_queries,
+              const ScanPlan& plan, void* partials, void* stream);
+
 }  // namespace dpf_amd

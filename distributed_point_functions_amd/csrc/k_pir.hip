@@ -203,7 +203,19 @@ __device__ __forceinline__ void FoldPartials(const ScanArgs& a, const uint4 (&ac
           r.z ^= x.z;
           r.w ^= x.w;
         }
-      a.partials[((int64_t)blockIdx.x * a.total_q + a.q0 + q) * a.C + chunk_lo + threadIdx.x] = r;
+      const int64_t part = a.slots ? (int64_t)(blockIdx.x % a.slots) : (int64_t)blockIdx.x;
+      uint4* dst = &a.partials[(part * a.total_q + a.q0 + q) * a.C + chunk_lo + threadIdx.x];
+      if (a.slots) {
+        // vector global atomics (per-lane addresses); XOR is order-free, so
+        // the folded result is the same bytes whatever order blocks finish in
+        unsigned int* d = reinterpret_cast<unsigned int*>(dst);
+        atomicXor(d + 0, r.x);
+        atomicXor(d + 1, r.y);
+        atomicXor(d + 2, r.z);
+        atomicXor(d + 3, r.w);
+      } else {
+        *dst = r;
+      }
     }
     __syncthreads();
   }

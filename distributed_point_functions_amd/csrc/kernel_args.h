@@ -140,8 +140,16 @@ struct ScanArgs {
   int32_t total_q;
   int32_t parts;        // partials written per query (KPirScanM4: waves in use)
   int32_t qgroups;      // KPirScanM4: waves scanning the same tiles (1 or 2)
-  int32_t pad;
+  // KPirScanG: 0 = one partial per block; S > 0 = block b XORs its partial
+  // atomically into partial slot b % S (zeroed before the scan), so the fold
+  // reads S partials instead of one per block.
+  int32_t slots;
 };
+
+// Fold slots of the masked scan when a pass's partial is small: 64 slots,
+// for at most kScanSlotMaxBytes of partial (queries x record bytes) per block.
+constexpr int kScanSlots = 64;
+constexpr int64_t kScanSlotMaxBytes = 2048;
 
 // KPirScanM4: 4 independent waves per block, one LDS table pair per wave.
 constexpr int kScanM4Block = 256;

@@ -488,7 +488,94 @@ int dpf_amd_evaluate_points_batched(int64_t num_keys, int64_t points_per_key,
 
 }  // extern "C"
 
+static int ScanGrid(int64_t num_records, int num_queries, int64_t record_stride) {
+  // At least one 128-record tile per wave; up to 8192 blocks / partials
+  // (c4 Q = 8: 2.95 ms vs 3.17 ms at 2048 — more, shorter blocks balance
+  // across CUs; KPirScanM4 at Q = 100: 2621 waves for 2048 resident slots
+  // left a 28 % second round), but at most 256 MiB of partials (grid x
+  // queries x record bytes) for the fold, and never fewer than 2048.
+  const int64_t tiles = (num_records + 127) / 128;
+  const int64_t g = (tiles + kScanWaves - 1) / kScanWaves;
+  const int64_t per_block = std::max<int64_t>(1, (int64_t)num_queries * record_stride);
+  const int64_t cap = std::max<int64_t>(2048, std::min<int64_t>(8192, (256ll << 20) / per_block));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+// Whether the next pass over `rem` queries of C-chunk records runs the
+// Four-Russians scan (KPirScanM4*) rather than the masked scan (KPirScanG).
+// Mode (dpf_amd_set_scan_m4 / DPF_AMD_SCAN_M4): 0 never, 1 always (tests),
+// -1 from kScanM4MinQueries queries on.
+static bool UseScanM4(int rem, int C) {
+  const int mode = t_scan_m4;
+  if (mode == 0) return false;
+  if (C > (1 << 16)) return false;  // records > 1 MiB: 128-record tiles past 2^27 B
+  if (mode < 0 && (rem < kScanM4MinQueries || C < 4)) return false;
+  return true;
+}
+
 namespace dpf_amd {
+// DPF_AMD_SCAN_SLOTS=0 (A/B): the masked scan always writes one partial per
+// block.
+static const bool kScanSlotsOn = [] {
+  const char* e = std::getenv("DPF_AMD_SCAN_SLOTS");
+  return !(e && std::atoi(e) == 0);
+}();
+
+ScanPlan PlanScan(int64_t num_records, int64_t record_stride, int num_queries) {
+  ScanPlan p;
+  p.grid = ScanGrid(num_records, num_queries, record_stride);
+  const int C = record_stride > 0 ? (int)(record_stride / 16) : 1;
+  // slots only when every pass is a masked pass (KPirScanM4 writes one
+  // partial per wave) and the block's partial is small
+  p.slots = kScanSlotsOn && num_queries > 0 && !UseScanM4(num_queries, C) &&
+            (int64_t)num_queries * record_stride <= kScanSlotMaxBytes && p.grid >= kScanSlots;
+  return p;
+}
+
+int ScanFoldParts(const ScanPlan& plan) { return plan.slots ? kScanSlots : plan.grid; }
+
+int ScanPiece(const void* db, int64_t num_records, int64_t record_stride,
+              const void* selections, int64_t selection_blocks, int num_queries,
+              const ScanPlan& plan, void* partials, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (num_queries == 0) return DPF_AMD_OK;
+  if (num_records < 0 || num_queries < 0)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "negative size");
+  if (record_stride <= 0 || record_stride % 16 != 0)
+    return SetError(DPF_AMD_INVALID_ARGUMENT, "record_stride must be a positive multiple of 16");
+  if (selection_blocks * 128 < num_records)
+    return SetError(DPF_AMD_INVALID_ARGUMENT,
+                    "`selections[0]` contains insufficient number of bits: " +
+                        std::to_string(selection_blocks * 128) +
+                        ", expected: " + std::to_string(num_records));
+  const int C = (int)(record_stride / 16);
+  const int per_pass = PirScanQueries(C);
+  const int grid = plan.grid;
+  ScanArgs a;
+  a.db = (const uint4*)db;
+  a.sel = (const uint4*)selections;
+  a.partials = (uint4*)partials;
+  a.num_records = num_records;
+  a.sel_blocks = selection_blocks;
+  a.C = C;
+  a.total_q = num_queries;
+  a.parts = grid;
+  a.qgroups = 1;
+  a.slots = plan.slots ? kScanSlots : 0;
+  const dim3 g(grid, (C + 63) / 64);
+  for (int q0 = 0; q0 < num_queries;) {
+    const int rem = num_queries - q0;
+    const bool m4 = !plan.slots && UseScanM4(rem, C);
+    const int nq = m4 ? PirScanM4Queries(rem) : std::min(per_pass, rem);
+    a.q0 = q0;
+    a.nq = nq;
+    int rc = m4 ? LaunchPirScanM4(nq, grid, (C + 15) / 16, st, a) : LaunchPirScan(nq, g, st, a);
+    if (rc != DPF_AMD_OK) return rc;
+    q0 += nq;
+  }
+  return DPF_AMD_OK;
+}
+
 int ExpandBatched(int64_t num_keys, const void* root_seeds, const uint8_t* root_cb,
                   int num_levels, const void* correction_seeds, const uint8_t* ccl,
                   const uint8_t* ccr, const dpf_amd_value_type* vt, const void* key_corr,
@@ -645,31 +732,6 @@ int dpf_amd_xor_fold(const void* parts, int num_parts, int64_t bytes, void* out,
                             bytes, (uint8_t*)out);
 }
 
-static int ScanGrid(int64_t num_records, int num_queries, int64_t record_stride) {
-  // At least one 128-record tile per wave; up to 8192 blocks / partials
-  // (c4 Q = 8: 2.95 ms vs 3.17 ms at 2048 — more, shorter blocks balance
-  // across CUs; KPirScanM4 at Q = 100: 2621 waves for 2048 resident slots
-  // left a 28 % second round), but at most 256 MiB of partials (grid x
-  // queries x record bytes) for the fold, and never fewer than 2048.
-  const int64_t tiles = (num_records + 127) / 128;
-  const int64_t g = (tiles + kScanWaves - 1) / kScanWaves;
-  const int64_t per_block = std::max<int64_t>(1, (int64_t)num_queries * record_stride);
-  const int64_t cap = std::max<int64_t>(2048, std::min<int64_t>(8192, (256ll << 20) / per_block));
-  return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
-}
-
-// Whether the next pass over `rem` queries of C-chunk records runs the
-// Four-Russians scan (KPirScanM4*) rather than the masked scan (KPirScanG).
-// Mode (dpf_amd_set_scan_m4 / DPF_AMD_SCAN_M4): 0 never, 1 always (tests),
-// -1 from kScanM4MinQueries queries on.
-static bool UseScanM4(int rem, int C) {
-  const int mode = t_scan_m4;
-  if (mode == 0) return false;
-  if (C > (1 << 16)) return false;  // records > 1 MiB: 128-record tiles past 2^27 B
-  if (mode < 0 && (rem < kScanM4MinQueries || C < 4)) return false;
-  return true;
-}
-
 int64_t dpf_amd_inner_product_workspace_size(int64_t num_records, int64_t record_stride,
                                              int num_queries) {
   return (int64_t)ScanGrid(num_records, num_queries, record_stride) * num_queries *
@@ -680,42 +742,20 @@ int dpf_amd_inner_product(const void* db, int64_t num_records, int64_t record_st
                           const void* selections, int64_t selection_blocks, int num_queries,
                           void* workspace, void* out, void* stream) {
   if (num_queries == 0) return DPF_AMD_OK;
-  if (num_records < 0 || num_queries < 0)
-    return SetError(DPF_AMD_INVALID_ARGUMENT, "negative size");
-  if (record_stride <= 0 || record_stride % 16 != 0)
-    return SetError(DPF_AMD_INVALID_ARGUMENT, "record_stride must be a positive multiple of 16");
-  if (selection_blocks * 128 < num_records)
-    return SetError(DPF_AMD_INVALID_ARGUMENT,
-                    "`selections[0]` contains insufficient number of bits: " +
-                        std::to_string(selection_blocks * 128) +
-                        ", expected: " + std::to_string(num_records));
+  const dpf_amd::ScanPlan plan = dpf_amd::PlanScan(num_records, record_stride, num_queries);
   hipStream_t st = (hipStream_t)stream;
-  const int C = (int)(record_stride / 16);
-  const int per_pass = PirScanQueries(C);
-  const int grid = ScanGrid(num_records, num_queries, record_stride);
-  ScanArgs a;
-  a.db = (const uint4*)db;
-  a.sel = (const uint4*)selections;
-  a.partials = (uint4*)workspace;
-  a.num_records = num_records;
-  a.sel_blocks = selection_blocks;
-  a.C = C;
-  a.total_q = num_queries;
-  a.parts = grid;
-  a.qgroups = 1;
-  a.pad = 0;
-  const dim3 g(grid, (C + 63) / 64);
-  for (int q0 = 0; q0 < num_queries;) {
-    const int rem = num_queries - q0;
-    const bool m4 = UseScanM4(rem, C);
-    const int nq = m4 ? PirScanM4Queries(rem) : std::min(per_pass, rem);
-    a.q0 = q0;
-    a.nq = nq;
-    int rc = m4 ? LaunchPirScanM4(nq, grid, (C + 15) / 16, st, a) : LaunchPirScan(nq, g, st, a);
+  if (plan.slots) {
+    int rc = HipCheck(hipMemsetAsync(workspace, 0, dpf_amd::ScanFoldParts(plan) *
+                                                       (int64_t)num_queries * record_stride,
+                                     st),
+                      "scan slots memset");
     if (rc != DPF_AMD_OK) return rc;
-    q0 += nq;
   }
-  return dpf_amd_xor_fold(workspace, grid, (int64_t)num_queries * record_stride, out, stream);
+  int rc = dpf_amd::ScanPiece(db, num_records, record_stride, selections, selection_blocks,
+                              num_queries, plan, workspace, stream);
+  if (rc != DPF_AMD_OK) return rc;
+  return dpf_amd_xor_fold(workspace, dpf_amd::ScanFoldParts(plan),
+                          (int64_t)num_queries * record_stride, out, stream);
 }
 
 }  // extern "C"

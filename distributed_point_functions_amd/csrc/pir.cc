@@ -295,21 +295,6 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductWithDevice(
   return r;
 }
 
-// Pieces per shard: DPF_AMD_PIR_SPLIT = k scans a shard as k 128-aligned row
-// ranges on k streams of its device, so one range's selection expansion can
-// run beside another's scan.  Measured on c4 (C++ HandleRequest, one box):
-// Q = 8 2.84 ms whole vs 3.01 in two pieces; Q = 64 6.43 vs 6.77 (two) and
-// 6.34 (four) — the scan's grid already fills the chip and each piece adds
-// its own tail and fold, so the default is one piece.
-int PiecesPerShard(int64_t rows) {
-  static const int forced = [] {
-    const char* e = std::getenv("DPF_AMD_PIR_SPLIT");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (forced > 1) return static_cast<int>(std::min<int64_t>(forced, std::max<int64_t>(1, rows / 128)));
-  return 1;
-}
-
 StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
     const FillSelectionsFn& fill, int num_queries) const {
   using dpf_internal_host::DeviceGuard;
@@ -317,73 +302,121 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
   if (num_queries == 0) return std::vector<std::string>();
   if (max_value_size_ <= 0) return InvalidArgumentError("`max_value_size` must be positive");
   const int64_t part_bytes = static_cast<int64_t>(num_queries) * stride_;
-  // Work pieces: each shard (or, with DPF_AMD_PIR_SPLIT, each of its
-  // 128-aligned row ranges) on a stream of its own — pieces on one device
-  // take consecutive stream indices, so shards that share a device overlap.
-  struct Work {
+  // Device groups: consecutive shards on one device with adjacent rows share
+  // one selection expansion (the group's block range), one workspace (the
+  // scans' partials side by side, or one set of atomic fold slots) and one
+  // fold — shards are per device, so on a node this is one group per GPU.
+  // With forced peer copies every shard is its own group, as if each sat on
+  // a device of its own (the rehearsal of the cross-device combine).
+  struct Piece {
     Shard sh;
+    dpf_amd::ScanPlan plan;
+    int64_t ws_off = 0;
+  };
+  struct Group {
+    int device = 0;
+    int64_t b0 = 0, b1 = 0;
+    std::vector<Piece> pieces;
     hipStream_t s = nullptr;
-    void* sel = nullptr;
-    void* ws = nullptr;
-    void* part = nullptr;
+    bool slots = true;
+    int fold_parts = 0;
+    void* buf = nullptr;
+    char* sel = nullptr;
+    char* ws = nullptr;
+    char* part = nullptr;
     hipEvent_t done = nullptr;
   };
-  std::vector<Work> w;
+  const bool force_peer = dpf_amd::ForcePeerCopies();
+  std::vector<Group> w;
   {
     std::map<int, int> next_index;
     for (const Shard& sh : shards_) {
-      const int64_t rows = sh.row_end - sh.row_begin;
-      const int k = PiecesPerShard(rows);
-      const int64_t per = ((rows + k - 1) / k + 127) / 128 * 128;
-      for (int p = 0; p < k; ++p) {
-        const int64_t r0 = sh.row_begin + p * per;
-        const int64_t r1 = std::min(sh.row_end, r0 + per);
-        if (r1 <= r0 && p > 0) break;
-        Work x;
-        x.sh = Shard{sh.device, r0, r1,
-                     static_cast<char*>(sh.records) + (r0 - sh.row_begin) * stride_};
-        x.s = dpf_internal_host::ThreadStreamOn(sh.device, next_index[sh.device]++);
-        w.push_back(x);
+      const int64_t b0 = sh.row_begin / 128, b1 = (sh.row_end + 127) / 128;
+      if (force_peer || w.empty() || w.back().device != sh.device || w.back().b1 != b0) {
+        Group g;
+        g.device = sh.device;
+        g.b0 = b0;
+        g.b1 = b0;
+        g.s = dpf_internal_host::ThreadStreamOn(sh.device, next_index[sh.device]++);
+        w.push_back(g);
       }
+      Group& g = w.back();
+      g.b1 = std::max(g.b1, b1);
+      Piece pc;
+      pc.sh = sh;
+      pc.plan = dpf_amd::PlanScan(sh.row_end - sh.row_begin, stride_, num_queries);
+      g.slots &= pc.plan.slots;
+      g.pieces.push_back(pc);
     }
   }
   const size_t G = w.size();
   dpf_internal_host::HostTrace trace("InnerProductSharded");
-  const int dev0 = shards_[0].device;
+  const int dev0 = w[0].device;
   hipStream_t s0 = w[0].s;
   void* gather = nullptr;
   void* folded = nullptr;
-  std::vector<char> host(part_bytes);
+  std::vector<char> host;
   Status st = OkStatus();
-  // 1. every piece: its selection blocks, then its scan, on its own stream
-  for (size_t g = 0; g < G && st.ok(); ++g) {
-    Work& x = w[g];
-    const Shard& sh = x.sh;
-    DeviceGuard dg(sh.device);
-    if (x.s == nullptr) {
-      st = InternalError("no stream on device " + std::to_string(sh.device));
+  // The last fold writes the answer straight into pinned host memory mapped
+  // into the device (no D2H copy behind it) when it is small.
+  void* hout = nullptr;
+  void* kout = nullptr;
+  if (part_bytes <= static_cast<int64_t>(dpf_internal_host::HostOutMax()))
+    st = dpf_internal_host::ThreadRecycled<dpf_internal_host::PinnedOut>::Get().Get(
+        part_bytes, &hout, &kout);
+  if (!kout) host.resize(part_bytes);
+  auto align = [](int64_t b) { return (b + 255) & ~int64_t{255}; };
+  // 1. every group: one allocation, its selection blocks, its scans and its
+  // fold, back to back on its own stream
+  for (size_t gi = 0; gi < G && st.ok(); ++gi) {
+    Group& g = w[gi];
+    DeviceGuard dg(g.device);
+    if (g.s == nullptr) {
+      st = InternalError("no stream on device " + std::to_string(g.device));
       break;
     }
-    const int64_t b0 = sh.row_begin / 128, b1 = (sh.row_end + 127) / 128;
-    const int64_t nb = std::max<int64_t>(1, b1 - b0);
-    const int64_t rows = sh.row_end - sh.row_begin;
-    st = DevicePool::Get().Alloc(16 * nb * num_queries, x.s, &x.sel);
-    if (st.ok()) st = fill(sh, b0, b1, x.sel, x.s);
+    const int64_t nb = std::max<int64_t>(1, g.b1 - g.b0);
+    int64_t ws_bytes = 0;
+    if (g.slots) {
+      g.fold_parts = dpf_amd::ScanFoldParts(g.pieces[0].plan);
+      ws_bytes = g.fold_parts * part_bytes;
+    } else {
+      for (Piece& pc : g.pieces) {
+        pc.plan.slots = false;
+        pc.ws_off = ws_bytes;
+        ws_bytes += dpf_amd::ScanFoldParts(pc.plan) * part_bytes;
+      }
+      g.fold_parts = static_cast<int>(ws_bytes / part_bytes);
+    }
+    const int64_t sel_bytes = align(16 * nb * num_queries);
+    const int64_t total = sel_bytes + align(std::max<int64_t>(16, ws_bytes)) + part_bytes;
+    st = DevicePool::Get().Alloc(total, g.s, &g.buf);
+    if (!st.ok()) break;
+    g.sel = static_cast<char*>(g.buf);
+    g.ws = g.sel + sel_bytes;
+    g.part = g.ws + align(std::max<int64_t>(16, ws_bytes));
+    if (g.slots)
+      st = HipStatus(hipMemsetAsync(g.ws, 0, ws_bytes, g.s), "scan slots memset");
+    if (st.ok()) st = fill(g.pieces[0].sh, g.b0, g.b0 + nb, g.sel, g.s);
+    for (size_t k = 0; k < g.pieces.size() && st.ok(); ++k) {
+      const Piece& pc = g.pieces[k];
+      const int64_t rows = pc.sh.row_end - pc.sh.row_begin;
+      const int64_t pb0 = pc.sh.row_begin / 128 - g.b0;
+      // query q's blocks of this piece: row q of the group's [query][nb]
+      st = AbiStatus(dpf_amd::ScanPiece(pc.sh.records, rows, stride_, g.sel + 16 * pb0, nb,
+                                        num_queries, pc.plan, g.ws + (g.slots ? 0 : pc.ws_off),
+                                        g.s));
+    }
     if (st.ok())
-      st = DevicePool::Get().Alloc(
-          std::max<int64_t>(16, dpf_amd_inner_product_workspace_size(rows, stride_, num_queries)),
-          x.s, &x.ws);
-    if (st.ok()) st = DevicePool::Get().Alloc(part_bytes, x.s, &x.part);
-    if (st.ok())
-      st = AbiStatus(dpf_amd_inner_product(sh.records, rows, stride_, x.sel, nb, num_queries,
-                                           x.ws, x.part, x.s));
+      st = AbiStatus(dpf_amd_xor_fold(g.ws, g.fold_parts, part_bytes,
+                                      G == 1 && kout ? kout : g.part, g.s));
     if (st.ok() && G > 1) {
-      st = HipStatus(hipEventCreateWithFlags(&x.done, hipEventDisableTiming), "hipEventCreate");
-      if (st.ok()) st = HipStatus(hipEventRecord(x.done, x.s), "hipEventRecord");
+      st = HipStatus(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "hipEventCreate");
+      if (st.ok()) st = HipStatus(hipEventRecord(g.done, g.s), "hipEventRecord");
     }
   }
   trace.Mark("selections+scan_launch");
-  // 2. combine on the first shard's device: (peer) copies of the partials,
+  // 2. combine on the first group's device: (peer) copies of the partials,
   // one XOR fold, one D2H
   const void* result = nullptr;
   if (st.ok()) {
@@ -397,19 +430,19 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
         char* dst = static_cast<char*>(gather) + g * part_bytes;
         st = HipStatus(hipStreamWaitEvent(s0, w[g].done, 0), "hipStreamWaitEvent");
         if (!st.ok()) break;
-        if (w[g].sh.device == dev0 && !dpf_amd::ForcePeerCopies())
+        if (w[g].device == dev0 && !force_peer)
           st = HipStatus(hipMemcpyAsync(dst, w[g].part, part_bytes, hipMemcpyDeviceToDevice, s0),
                          "partials copy");
         else
-          st = HipStatus(hipMemcpyPeerAsync(dst, dev0, w[g].part, w[g].sh.device, part_bytes,
-                                            s0),
+          st = HipStatus(hipMemcpyPeerAsync(dst, dev0, w[g].part, w[g].device, part_bytes, s0),
                          "partials peer copy");
       }
       if (st.ok())
-        st = AbiStatus(dpf_amd_xor_fold(gather, static_cast<int>(G), part_bytes, folded, s0));
+        st = AbiStatus(dpf_amd_xor_fold(gather, static_cast<int>(G), part_bytes,
+                                        kout ? kout : folded, s0));
       result = folded;
     }
-    if (st.ok())
+    if (st.ok() && !kout)
       st = HipStatus(hipMemcpyAsync(host.data(), result, part_bytes, hipMemcpyDeviceToHost, s0),
                      "d2h");
   }
@@ -417,7 +450,7 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
   // 3. drain every stream used, then return the buffers (no copy still reads them)
   for (size_t g = 0; g < G; ++g) {
     if (!w[g].s) continue;
-    DeviceGuard dg(w[g].sh.device);
+    DeviceGuard dg(w[g].device);
     Status sy = HipStatus(hipStreamSynchronize(w[g].s), "sync");
     if (st.ok()) st = sy;
   }
@@ -429,15 +462,15 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
     if (folded) DevicePool::Get().Free(folded, s0);
   }
   for (size_t g = 0; g < G; ++g) {
-    DeviceGuard dg(w[g].sh.device);
-    for (void* p : {w[g].sel, w[g].ws, w[g].part})
-      if (p) DevicePool::Get().Free(p, w[g].s);
+    DeviceGuard dg(w[g].device);
+    if (w[g].buf) DevicePool::Get().Free(w[g].buf, w[g].s);
     if (w[g].done) (void)hipEventDestroy(w[g].done);
   }
   trace.Mark("sync+free");
   if (!st.ok()) return st;
+  const char* answer = kout ? static_cast<const char*>(hout) : host.data();
   std::vector<std::string> r(num_queries);
-  for (int q = 0; q < num_queries; ++q) r[q].assign(host.data() + q * stride_, max_value_size_);
+  for (int q = 0; q < num_queries; ++q) r[q].assign(answer + q * stride_, max_value_size_);
   return r;
 }
 

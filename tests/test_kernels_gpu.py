@@ -359,7 +359,12 @@ SCAN_CASES = [(1, 16, 1), (1000, 256, 1), (1000, 256, 3), (4096, 80, 8), (300, 1
               # queries per pass), ragged tiles, several 256-B slices, a
               # narrow last slice (1104 B = 4 x 256 + 80), 100 queries
               (1000, 256, 17), (3001, 256, 32), (4097, 512, 33), (130, 256, 64),
-              (2500, 768, 100), (2049, 1104, 40), (640, 240, 16), (385, 64, 9)]
+              (2500, 768, 100), (2049, 1104, 40), (640, 240, 16), (385, 64, 9),
+              # >= 64 scan blocks with a partial of <= 2 KiB: the masked scan
+              # XORs block partials into 64 atomic fold slots (ragged last
+              # tile, two 64-chunk slices at 1104 B, Q x 256 B = 2 KiB)
+              (40000, 256, 1), (33001, 48, 3), (36001, 1104, 1), (50000, 256, 8),
+              (40000, 16, 5)]
 
 
 def _scan_case(K, cuda, n, size, q, mode):
@@ -398,7 +403,10 @@ def test_inner_product_each_scan_kernel(K, cuda, n, size, q, mode):
 
 
 @pytest.mark.parametrize("n,size,qs", [(1 << 22, 256, (16, 40, 64, 100)),
-                                       (1 << 18, 1104, (33,))])
+                                       (1 << 18, 1104, (33,)),
+                                       # masked scan with atomic fold slots
+                                       # vs the Four-Russians partials
+                                       (1 << 22, 256, (1, 8)), (1 << 20, 1104, (1,))])
 def test_scan_kernels_agree_large(K, cuda, n, size, qs):
     """Random full selections over millions of records: the Four-Russians
     scan equals the masked scan (each pinned to the oracle above) and repeats
