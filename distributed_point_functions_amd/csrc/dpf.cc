@@ -1008,7 +1008,7 @@ Status ValidateEvaluationContext(const DpfState& st, const EvaluationContext& ct
     return InvalidArgumentError("ctx.previous_hierarchy_level out of range");
   if (ctx.partial_evaluations_level() < 0 || ctx.partial_evaluations_level() >= num_levels)
     return InvalidArgumentError("ctx.partial_evaluations_level out of range");
-  if (!ctx.partial_evaluations().empty() &&
+  if (ctx.partial_evaluations_size() > 0 &&
       ctx.partial_evaluations_level() > ctx.previous_hierarchy_level())
     return InvalidArgumentError(
         "ctx.partial_evaluations_level must be less than or equal to "
@@ -1073,6 +1073,91 @@ StatusOr<EvaluationContext> DistributedPointFunction::CreateEvaluationContext(Dp
 }
 
 // --- evaluation --------------------------------------------------------------
+
+// The partial evaluations of an EvaluationContext kept in HBM between
+// EvaluateUntil calls: the previous level's unique tree
+// indices (strictly increasing), their walked seeds and control bits, in one
+// pool block on `device`.  EvaluateUntil's device path looks its prefixes up
+// here; a caller reading the context's field gets host messages built once.
+class ContextDeviceState {
+ public:
+  ~ContextDeviceState() {
+    if (buf_ == nullptr) return;
+    dpf_internal_host::DeviceGuard g(device_);
+    dpf_internal_host::DevicePool::Get().Free(buf_, stream_);
+  }
+  static Status Create(int64_t capacity, hipStream_t s, std::shared_ptr<ContextDeviceState>* out) {
+    auto st = std::shared_ptr<ContextDeviceState>(new ContextDeviceState());
+    DPF_RETURN_IF_ERROR(HipStatus(hipGetDevice(&st->device_), "hipGetDevice"));
+    st->stream_ = s;
+    const int64_t n = std::max<int64_t>(1, capacity);
+    const int64_t bytes = 32 * n + ((n + 15) & ~int64_t{15}) + 16;
+    DPF_RETURN_IF_ERROR(dpf_internal_host::DevicePool::Get().Alloc(bytes, s, &st->buf_));
+    char* b = static_cast<char*>(st->buf_);
+    st->prefixes_ = b;
+    st->seeds_ = b + 16 * n;
+    st->cbs_ = reinterpret_cast<uint8_t*>(b + 32 * n);
+    st->count_dev_ = reinterpret_cast<int64_t*>(b + 32 * n + ((n + 15) & ~int64_t{15}));
+    *out = std::move(st);
+    return OkStatus();
+  }
+  int device() const { return device_; }
+  char* prefixes() const { return prefixes_; }
+  char* seeds() const { return seeds_; }
+  uint8_t* cbs() const { return cbs_; }
+  int64_t* count_dev() const { return count_dev_; }
+  int64_t count() const { return count_; }
+  void set_count(int64_t c) { count_ = c; }
+  void set_stream(hipStream_t s) { stream_ = s; }
+
+  // The list as host messages, read back on first use (the kernels that
+  // wrote it finished before the state was attached to a context).
+  const std::vector<PartialEvaluation>& Host() const {
+    std::call_once(once_, [this] {
+      const size_t n = static_cast<size_t>(count_);
+      std::vector<uint128> p(n), sd(n);
+      std::vector<uint8_t> cb(n);
+      dpf_internal_host::DeviceGuard g(device_);
+      if (n == 0 ||
+          hipMemcpy(p.data(), prefixes_, 16 * n, hipMemcpyDeviceToHost) != hipSuccess ||
+          hipMemcpy(sd.data(), seeds_, 16 * n, hipMemcpyDeviceToHost) != hipSuccess ||
+          hipMemcpy(cb.data(), cbs_, n, hipMemcpyDeviceToHost) != hipSuccess) {
+        (void)hipGetLastError();
+        return;  // an unreadable list reads as empty: later lookups report it missing
+      }
+      host_.resize(n);
+      for (size_t i = 0; i < n; ++i) {
+        PartialEvaluation& x = host_[i];
+        x.mutable_prefix()->set_high(Uint128High64(p[i]));
+        x.mutable_prefix()->set_low(Uint128Low64(p[i]));
+        x.mutable_seed()->set_high(Uint128High64(sd[i]));
+        x.mutable_seed()->set_low(Uint128Low64(sd[i]));
+        x.set_control_bit(cb[i] != 0);
+      }
+    });
+    return host_;
+  }
+
+ private:
+  ContextDeviceState() = default;
+  int device_ = 0;
+  hipStream_t stream_ = nullptr;
+  void* buf_ = nullptr;
+  char* prefixes_ = nullptr;
+  char* seeds_ = nullptr;
+  uint8_t* cbs_ = nullptr;
+  int64_t* count_dev_ = nullptr;
+  int64_t count_ = 0;
+  mutable std::once_flag once_;
+  mutable std::vector<PartialEvaluation> host_;
+};
+
+const std::vector<PartialEvaluation>& PartialEvaluationsOf(const ContextDeviceState& state) {
+  return state.Host();
+}
+int PartialEvaluationsCountOf(const ContextDeviceState& state) {
+  return static_cast<int>(state.count());
+}
 
 namespace {
 
@@ -1155,6 +1240,8 @@ IncrementalScratch& ThreadScratch() {
 // filled over the host pool: 2^16 entries per c3 level.
 void RewritePartialEvaluations(EvaluationContext& ctx, const uint128* prefixes,
                                const uint128* seeds, const uint8_t* cbs, int64_t n) {
+  // a device-held list is replaced, not read back first
+  if (ctx.device_state()) ctx.set_device_state(nullptr);
   std::vector<PartialEvaluation>* pe = ctx.mutable_partial_evaluations();
   pe->resize(n);
   HostPool::Get().ParallelRanges(n, 8192, [&](int, int64_t b, int64_t e) {
@@ -1392,6 +1479,158 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
   return OkStatus();
 }
 
+// EvaluateUntil with prefixes, on the device end to end:
+// the prefixes go up once; their de-duplication, the range and order checks,
+// the lookup of the stored partial evaluations (ComputePartialEvaluations,
+// cc:374-476) and the walk run as kernels; the walked unique tree indices stay
+// in HBM as the context's new list (a ContextDeviceState).  Sets *fallback
+// (and leaves ctx as it was) when the host path must run instead: a context
+// whose list is on the host or another device, unsorted prefixes, a prefix
+// out of range or not in the list — the host path then gives the reference's
+// result or error.
+Status EvaluateUntilOnDevice(const DpfState& st, int hierarchy_level,
+                             Span<const uint128> prefixes, EvaluationContext& ctx,
+                             const dpf_amd_value_type& vt, const std::vector<uint128>& corr,
+                             void* out, bool out_on_device, hipStream_t s, bool* fallback) {
+  *fallback = true;
+  HostTrace trace("EvaluateUntilOnDevice");
+  const int L = static_cast<int>(st.parameters.size());
+  const int prev_h = ctx.previous_hierarchy_level();
+  const int prev_ld = st.parameters[prev_h].log_domain_size();
+  const int prev_tree = st.hierarchy_to_tree[prev_h];
+  const int stop_level = st.hierarchy_to_tree[hierarchy_level];
+  const int log_domain_size = st.parameters[hierarchy_level].log_domain_size();
+  const int bbits = prev_ld - prev_tree;  // prefix bits below its tree index (< 8)
+  const int64_t n = static_cast<int64_t>(prefixes.size());
+  if (n == 0 || n >= (int64_t{1} << 31) || bbits > 7 || stop_level < prev_ld) return OkStatus();
+  int cur_dev = 0;
+  DPF_RETURN_IF_ERROR(HipStatus(hipGetDevice(&cur_dev), "hipGetDevice"));
+  // where the walk starts: the stored list (device-held, this device) or the root
+  std::shared_ptr<const ContextDeviceState> old = ctx.device_state();
+  bool from_root = true;
+  int start_level = 0;
+  if (old) {
+    if (old->device() != cur_dev) return OkStatus();
+    const int pe_level = ctx.partial_evaluations_level();
+    const int sl = st.hierarchy_to_tree[pe_level];
+    if (old->count() > 0 && sl <= prev_tree) {
+      from_root = false;
+      start_level = sl;
+    }
+  } else if (ctx.partial_evaluations_size() > 0) {
+    return OkStatus();  // a host-held list (a parsed or host-path context)
+  }
+  const int walk_levels = prev_tree - start_level;
+  const int down = stop_level - prev_ld;
+  const int cepb = 1 << (log_domain_size - stop_level);
+  const int64_t outputs_per_prefix = int64_t{1} << (log_domain_size - prev_ld);
+  const int64_t total = n * outputs_per_prefix;
+  const size_t stride = static_cast<size_t>(vt.out_stride);
+  const bool update_ctx = hierarchy_level < L - 1;
+
+  // work buffer: prefixes | prefix index | low bits | dedup block counts |
+  // flags | correction words (walk, prefix roots, expansion) | prefix roots
+  CwArrays kc = KeyCws(ctx.key(), start_level, prev_tree);
+  CwArrays wc = KeyCws(ctx.key(), prev_tree, prev_ld);
+  CwArrays ec = KeyCws(ctx.key(), prev_ld, stop_level);
+  using Part = UploadRing::HostPart;
+  const Part parts[9] = {{kc.seeds.data(), size_t(16) * walk_levels},
+                         {kc.ccl.data(), size_t(walk_levels)},
+                         {kc.ccr.data(), size_t(walk_levels)},
+                         {wc.seeds.data(), size_t(16) * bbits},
+                         {wc.ccl.data(), size_t(bbits)},
+                         {wc.ccr.data(), size_t(bbits)},
+                         {ec.seeds.data(), size_t(16) * down},
+                         {ec.ccl.data(), size_t(down)},
+                         {ec.ccr.data(), size_t(down)}};
+  size_t coff[9];
+  const size_t cw_bytes = UploadRing::PackedLayout(parts, 9, coff);
+  auto al = [](size_t b) { return (b + 255) & ~size_t{255}; };
+  const size_t o_p = 0;
+  const size_t o_idx = o_p + al(16 * size_t(n));
+  const size_t o_low = o_idx + al(4 * size_t(n));
+  const size_t o_blk = o_low + al(size_t(n));
+  const size_t o_flags = o_blk + al(8 * size_t(dpf_amd::DedupBlocks(n)));
+  const size_t o_cw = o_flags + 256;
+  const size_t o_ps = o_cw + al(cw_bytes);
+  const size_t o_pcb = o_ps + al(16 * size_t(n));
+  const size_t o_out = o_pcb + al(size_t(n));
+  DeviceBuffer work;
+  DPF_RETURN_IF_ERROR(work.Alloc(o_out + (out_on_device ? 0 : total * stride), s));
+  char* w = work.as<char>();
+  std::shared_ptr<ContextDeviceState> next;
+  DPF_RETURN_IF_ERROR(ContextDeviceState::Create(n, s, &next));
+  IncrementalScratch& sc = ThreadScratch();
+  if (sc.done) DPF_RETURN_IF_ERROR(HipStatus(hipEventSynchronize(sc.done), "d2h"));
+  DPF_RETURN_IF_ERROR(sc.Reserve(1));
+  int64_t* readback = reinterpret_cast<int64_t*>(sc.flag);  // pinned: flags, count
+  readback[0] = readback[1] = 0;
+  // an early error return must not leave an async copy into `readback` in flight
+  StreamSyncGuard drain(s);
+  trace.Mark("setup");
+  int* flags = reinterpret_cast<int*>(w + o_flags);
+  DPF_RETURN_IF_ERROR(HipStatus(hipMemsetAsync(flags, 0, sizeof(int), s), "hipMemsetAsync"));
+  DPF_RETURN_IF_ERROR(ThreadUploadRing().Copy(w + o_p, prefixes.data(), 16 * size_t(n), s));
+  DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(w + o_cw, parts, 9, cw_bytes, coff, s));
+  trace.Mark("upload");
+  const uint64_t limit[2] = {prev_ld < 64 ? (uint64_t{1} << prev_ld) : 0,
+                             prev_ld >= 64 && prev_ld < 128 ? (uint64_t{1} << (prev_ld - 64)) : 0};
+  int32_t* pidx = reinterpret_cast<int32_t*>(w + o_idx);
+  uint8_t* plow = reinterpret_cast<uint8_t*>(w + o_low);
+  DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd::DedupPrefixes(
+      w + o_p, n, bbits, prev_ld < 128 ? limit : nullptr, pidx, plow, next->prefixes(),
+      next->count_dev(), reinterpret_cast<int64_t*>(w + o_blk), flags, s)));
+  const uint64_t root[2] = {ctx.key().seed().low(), ctx.key().seed().high()};
+  DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd::LookupPartialEvaluations(
+      next->prefixes(), next->count_dev(), n, prev_tree - start_level,
+      from_root ? nullptr : old->prefixes(), from_root ? 0 : old->count(),
+      from_root ? nullptr : old->seeds(), from_root ? nullptr : old->cbs(), root,
+      ctx.key().party() != 0, from_root, next->seeds(), next->cbs(), flags, s)));
+  // the walk of every unique tree index to the previous level's tree level
+  // (entries past the count are walked too: unused, and n bounds them)
+  if (walk_levels > 0)
+    DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_seeds(
+        n, walk_levels, walk_levels, next->seeds(), next->cbs(), next->prefixes(), 0,
+        w + o_cw + coff[0], reinterpret_cast<const uint8_t*>(w + o_cw + coff[1]),
+        reinterpret_cast<const uint8_t*>(w + o_cw + coff[2]), dpf_amd::kPrgKeyLeftLo,
+        dpf_amd::kPrgKeyLeftHi, dpf_amd::kPrgKeyRightLo, dpf_amd::kPrgKeyRightHi, next->seeds(),
+        next->cbs(), s)));
+  // each prefix's own node, then its subtree (as the host path's fused branch)
+  DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd::PrefixRoots(
+      n, pidx, plow, bbits, n, next->seeds(), next->cbs(), w + o_cw + coff[3],
+      reinterpret_cast<const uint8_t*>(w + o_cw + coff[4]),
+      reinterpret_cast<const uint8_t*>(w + o_cw + coff[5]), w + o_ps,
+      reinterpret_cast<uint8_t*>(w + o_pcb), s)));
+  void* final_dev = out_on_device ? out : static_cast<void*>(w + o_out);
+  DPF_RETURN_IF_ERROR(ClearPadding(vt, final_dev, total * stride, s));
+  DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_expand_and_correct(
+      n, w + o_ps, reinterpret_cast<const uint8_t*>(w + o_pcb), down, w + o_cw + coff[6],
+      reinterpret_cast<const uint8_t*>(w + o_cw + coff[7]),
+      reinterpret_cast<const uint8_t*>(w + o_cw + coff[8]), &vt,
+      reinterpret_cast<const uint64_t*>(corr.data()), ctx.key().party(), cepb, 0, n << down,
+      final_dev, s)));
+  DPF_RETURN_IF_ERROR(CopyToHost(readback, flags, sizeof(int), s));
+  DPF_RETURN_IF_ERROR(CopyToHost(readback + 1, next->count_dev(), sizeof(int64_t), s));
+  trace.Mark("launch");
+  if (!out_on_device)
+    DPF_RETURN_IF_ERROR(CopyToHostSync(out, final_dev, total * stride, s));
+  else
+    DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+  drain.Dismiss();
+  trace.Mark("sync");
+  if (readback[0] != 0) return OkStatus();  // the host path decides
+  *fallback = false;
+  if (update_ctx) {
+    next->set_count(readback[1]);
+    ctx.set_device_state(std::move(next));
+  } else {
+    ctx.clear_partial_evaluations();
+  }
+  ctx.set_partial_evaluations_level(prev_h);
+  ctx.set_previous_hierarchy_level(hierarchy_level);
+  return OkStatus();
+}
+
 }  // namespace
 
 Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
@@ -1433,8 +1672,10 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
                                     " out of range for hierarchy level " + std::to_string(prev_h));
     return OkStatus();
   };
+  // (the size query, out == nullptr, leaves the check to the evaluation
+  // call that follows it)
   const bool range_deferred =
-      out != nullptr && static_cast<int64_t>(prefixes.size()) >= (int64_t{1} << 14);
+      out == nullptr || static_cast<int64_t>(prefixes.size()) >= (int64_t{1} << 14);
   if (!range_deferred) DPF_RETURN_IF_ERROR(range_check());
   auto early = [&](Status e) -> Status {
     if (range_deferred) DPF_RETURN_IF_ERROR(range_check());
@@ -1466,6 +1707,14 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   }
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ThreadStream();
   trace.Mark("corrections");
+  if (!prefixes.empty() && !dpf_amd::HostIncremental() && !dpf_amd::PrefixExpandOff()) {
+    bool fallback = true;
+    Status e = EvaluateUntilOnDevice(st, hierarchy_level, prefixes, ctx, vt, corr, out,
+                                     out_on_device, s, &fallback);
+    if (!e.ok()) return early(e);
+    if (!fallback) return OkStatus();
+    trace.Mark("device_path_declined");
+  }
 
   // Unique tree indices in first-appearance order (h:772-796), and each
   // prefix's gather offset into the expansion (h:877-889).  Sorted prefixes
@@ -1845,11 +2094,13 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
     trace.Mark("launch");
     if (host_out) {
       DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+      trace.Mark("sync");
       std::memcpy(out, hout, out_bytes);
+      trace.Mark("copy_out");
     } else {
       DPF_RETURN_IF_ERROR(CopyToHostSync(out, kout, out_bytes, s));
+      trace.Mark("d2h+sync");
     }
-    trace.Mark("d2h+sync");
     return OkStatus();
   }
   // With a context: the stored partial evaluations are walked to this

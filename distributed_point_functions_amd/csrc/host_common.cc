@@ -92,7 +92,7 @@ std::atomic<int> g_thread_cache_cap{[] {
   return e ? atoi(e) : 64;
 }()};
 std::atomic<int> g_force_peer_copies{0};
-thread_local int t_prefix_expand = 0;  // 0 automatic, 1 off
+thread_local int t_prefix_expand = 0;  // 0 automatic, 1 off, 2 host bookkeeping
 }  // namespace
 
 int ThreadCacheCap() { return g_thread_cache_cap.load(std::memory_order_relaxed); }
@@ -103,6 +103,13 @@ bool PrefixExpandOff() {
     return e && atoi(e) == 0;
   }();
   return env_off || t_prefix_expand == 1;
+}
+bool HostIncremental() {
+  static const bool env_host = [] {
+    const char* e = getenv("DPF_AMD_HOST_INCREMENTAL");
+    return e && atoi(e) != 0;
+  }();
+  return env_host || t_prefix_expand == 2;
 }
 
 }  // namespace dpf_amd
@@ -122,7 +129,7 @@ int dpf_amd_set_thread_cache_cap(int cap) {
 void dpf_amd_set_force_peer_copies(int on) { dpf_amd::g_force_peer_copies.store(on ? 1 : 0); }
 
 int dpf_amd_set_prefix_expand(int mode) {
-  if (mode < 0 || mode > 1) return -2;
+  if (mode < 0 || mode > 2) return -2;
   const int prev = dpf_amd::t_prefix_expand;
   dpf_amd::t_prefix_expand = mode;
   return prev;

@@ -274,8 +274,9 @@ class HostPool {
     });
     return static_cast<int>(parts);
   }
-  void Copy(char* dst, const char* src, size_t bytes) {
-    const size_t parts = std::min<size_t>(kWorkers + 1, std::max<size_t>(1, bytes >> 20));
+  // memcpy split over the pool in pieces of at least `grain` bytes
+  void Copy(char* dst, const char* src, size_t bytes, size_t grain = size_t{1} << 20) {
+    const size_t parts = std::min<size_t>(kWorkers + 1, std::max<size_t>(1, bytes / grain));
     const size_t per = (bytes + parts - 1) / parts;
     Run(parts, [&](size_t i) {
       const size_t off = i * per;

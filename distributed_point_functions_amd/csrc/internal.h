@@ -21,6 +21,10 @@ bool ForcePeerCopies();
 // dpf_amd_set_prefix_expand / DPF_AMD_PREFIX_EXPAND=0: EvaluateUntil expands
 // unique tree indices and gathers, instead of expanding per prefix.
 bool PrefixExpandOff();
+// dpf_amd_set_prefix_expand(2) / DPF_AMD_HOST_INCREMENTAL=1: EvaluateUntil
+// keeps the prefix de-duplication, the lookup of the stored partial
+// evaluations and the context on the host (the device path's A/B).
+bool HostIncremental();
 
 // Device-side copy of dpf_amd_value_type plus everything the per-leaf
 // correction needs (kernel argument, < 2 KiB).
@@ -107,6 +111,26 @@ int EvaluatePointsIndexed(int64_t num_points, const int32_t* key_index, int64_t 
 int PrefixRoots(int64_t n, const int32_t* idx, const uint8_t* low, int walk, int64_t num_src,
                 const void* seeds, const uint8_t* cb, const void* cw_seed, const uint8_t* ccl,
                 const uint8_t* ccr, void* seeds_out, uint8_t* cb_out, void* stream);
+
+// EvaluateUntil's prefix bookkeeping on the device (k_incremental.hip).
+// DedupPrefixes: n (< 2^31) sorted 128-bit prefixes -> their unique tree
+// indices p >> bbits in order (`unique`, *count of them), prefix i's unique
+// index pidx[i] and low bits plow[i] = p & (2^bbits - 1); *flags |= 1 when
+// the prefixes are not sorted, 2 when one is >= limit ({lo, hi}; none when
+// null).  block_scratch holds DedupBlocks(n) int64.  LookupPartialEvaluations:
+// unique index u < min(*count, n_max) -> the stored partial evaluation of
+// unique[u] >> shift (binary search of the strictly increasing stored list)
+// or, from_root, the key's root seed / control bit; *flags |= 4 when one is
+// missing.  Device pointers, stream-ordered.
+int64_t DedupBlocks(int64_t n);
+int DedupPrefixes(const void* prefixes, int64_t n, int bbits, const uint64_t* limit,
+                  int32_t* pidx, uint8_t* plow, void* unique, int64_t* count,
+                  int64_t* block_scratch, int* flags, void* stream);
+int LookupPartialEvaluations(const void* unique, const int64_t* count, int64_t n_max, int shift,
+                             const void* stored, int64_t stored_n, const void* stored_seeds,
+                             const uint8_t* stored_cb, const uint64_t root_seed[2], int root_cb,
+                             bool from_root, void* seeds_out, uint8_t* cb_out, int* flags,
+                             void* stream);
 
 // Dense-PIR scan of one database piece, split from its fold so several
 // pieces on one device can share one workspace and one fold

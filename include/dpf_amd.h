@@ -197,9 +197,11 @@ int dpf_amd_set_walk_mode(int mode);
 /* Test hook: the calling thread's EvaluateUntil strategy for calls with
  * prefixes.  0 = automatic (each prefix's own subtree expanded straight into
  * the output when this level's tree level is at or below the prefix's
- * depth), 1 = the unique tree indices expanded into a staging buffer and
- * gathered per prefix (h:772-889's shape).  Returns the previous setting, or
- * -2 for an invalid mode (unchanged). */
+ * depth, with the de-duplication, the lookup of the stored partial
+ * evaluations and the context's list kept on the device), 1 = the unique
+ * tree indices expanded into a staging buffer and gathered per prefix
+ * (h:772-889's shape), 2 = as 0 with that bookkeeping on the host.  Returns
+ * the previous setting, or -2 for an invalid mode (unchanged). */
 int dpf_amd_set_prefix_expand(int mode);
 
 /* Test hook: the calling thread's DCF BatchEvaluate kernel.  0 = automatic

@@ -9,6 +9,7 @@
 
 #include <stdint.h>
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -239,24 +240,71 @@ class PartialEvaluation {
   bool control_bit_ = false;
 };
 
+// The partial evaluations EvaluateUntil left on a GPU (library-internal,
+// defined in the library): the list is read back into host messages only
+// when a caller reads the field, once per list.
+class ContextDeviceState;
+const std::vector<PartialEvaluation>& PartialEvaluationsOf(const ContextDeviceState& state);
+int PartialEvaluationsCountOf(const ContextDeviceState& state);
+
 class EvaluationContext {
  public:
   DPF_AMD_REPEATED_FIELD(DpfParameters, parameters)
   DPF_AMD_MESSAGE_FIELD(DpfKey, key)
   DPF_AMD_SCALAR_FIELD(int32_t, previous_hierarchy_level)
-  DPF_AMD_REPEATED_FIELD(PartialEvaluation, partial_evaluations)
+  // repeated PartialEvaluation partial_evaluations (proto field 4): reads
+  // see the device-held list when there is one; writes take it to the host
+  int partial_evaluations_size() const {
+    return device_ ? PartialEvaluationsCountOf(*device_)
+                   : static_cast<int>(partial_evaluations_.size());
+  }
+  const PartialEvaluation& partial_evaluations(int i) const { return partial_evaluations()[i]; }
+  const std::vector<PartialEvaluation>& partial_evaluations() const {
+    return device_ ? PartialEvaluationsOf(*device_) : partial_evaluations_;
+  }
+  PartialEvaluation* mutable_partial_evaluations(int i) {
+    ToHost();
+    return &partial_evaluations_[i];
+  }
+  std::vector<PartialEvaluation>* mutable_partial_evaluations() {
+    ToHost();
+    return &partial_evaluations_;
+  }
+  PartialEvaluation* add_partial_evaluations() {
+    ToHost();
+    partial_evaluations_.emplace_back();
+    return &partial_evaluations_.back();
+  }
+  void clear_partial_evaluations() {
+    device_.reset();
+    partial_evaluations_.clear();
+  }
   DPF_AMD_SCALAR_FIELD(int32_t, partial_evaluations_level)
 
   std::string SerializeAsString() const;
   bool ParseFromString(const std::string& data);
   bool ParseFromArray(const void* data, size_t size);
 
+  // Library-internal: the device-held partial evaluations (null when the
+  // list is on the host).  Setting one replaces the host list.
+  const std::shared_ptr<const ContextDeviceState>& device_state() const { return device_; }
+  void set_device_state(std::shared_ptr<const ContextDeviceState> state) {
+    partial_evaluations_.clear();
+    device_ = std::move(state);
+  }
+
  private:
+  void ToHost() {
+    if (!device_) return;
+    partial_evaluations_ = PartialEvaluationsOf(*device_);
+    device_.reset();
+  }
   std::vector<DpfParameters> parameters_;
   bool has_key_ = false;
   DpfKey key_;
   int32_t previous_hierarchy_level_ = 0;
   std::vector<PartialEvaluation> partial_evaluations_;
+  std::shared_ptr<const ContextDeviceState> device_;
   int32_t partial_evaluations_level_ = 0;
 };
 

@@ -112,14 +112,16 @@ def test_walk_and_dcf_kernel_hooks_validate_and_are_per_thread():
 
 
 def test_prefix_expand_and_thread_cache_hooks():
-    """dpf_amd_set_prefix_expand (0 / 1) is per thread and refuses other
+    """dpf_amd_set_prefix_expand (0 / 1 / 2) is per thread and refuses other
     values; dpf_amd_set_thread_cache_cap refuses a negative cap (no GPU: the
     setters touch no device state)."""
     import threading
     from distributed_point_functions_amd import _lib
     L = _lib.lib()
-    assert L.dpf_amd_set_prefix_expand(2) == -2
-    assert L.dpf_amd_set_prefix_expand(1) == 0
+    assert L.dpf_amd_set_prefix_expand(3) == -2
+    assert L.dpf_amd_set_prefix_expand(-1) == -2
+    assert L.dpf_amd_set_prefix_expand(2) == 0
+    assert L.dpf_amd_set_prefix_expand(1) == 2
     seen = {}
 
     def other():

@@ -69,11 +69,13 @@ def _evaluator(dpf, od, hier, ctxs, octxs):
     return evaluate
 
 
-@pytest.fixture(params=[0, 1], ids=["prefix_expand", "unique_expand_gather"])
+@pytest.fixture(params=[0, 1, 2], ids=["prefix_expand", "unique_expand_gather", "host_bookkeeping"])
 def expand_mode(request, api):
-    """EvaluateUntil's two strategies for calls with prefixes
+    """EvaluateUntil's strategies for calls with prefixes
     (dpf_amd_set_prefix_expand): each prefix's subtree expanded straight into
-    the output, or the unique tree indices expanded and gathered."""
+    the output with the de-duplication, the context lookup and the context's
+    list on the device (0) or on the host (2), or the unique tree indices
+    expanded and gathered (1)."""
     from distributed_point_functions_amd import _lib
     L = _lib.lib()
     prev = L.dpf_amd_set_prefix_expand(request.param)
@@ -187,3 +189,69 @@ def test_evaluate_at_ctx_errors(api):
         dpf.evaluate_at_ctx(1, [256], ctx)
     assert "`evaluation_points[0]` larger than the domain size at hierarchy level 1" in str(e.value)
     assert dpf.evaluate_at_ctx(1, [], ctx) == []
+
+
+def test_device_bookkeeping_equals_host_path(api):
+    """EvaluateUntil's device path (de-duplication, stored-evaluation lookup
+    and the context's list in HBM, dpf_amd_set_prefix_expand(0)) against the
+    host path (mode 2): identical outputs and identical serialized contexts
+    at every level — sorted prefixes with duplicates, a context copied
+    through its wire bytes midway (its list then on the host), unsorted
+    prefixes (the device path declines, the host path's hash lookup runs) —
+    and the reference's errors for a prefix outside the domain and one the
+    context never evaluated."""
+    from distributed_point_functions_amd import _lib
+    from distributed_point_functions_amd._lib import DpfAmdError
+    L = _lib.lib()
+    lds = [8, 16, 24, 32, 40, 48]
+    levels = [(ld, ("int", 64), 0) for ld in lds]
+    dpf = _make(api, levels)
+    rng = np.random.default_rng(55)
+    alpha = int(rng.integers(0, 1 << 48))
+    keys = dpf.generate_keys_incremental(alpha, [3 + i for i in range(len(lds))], seeds=(4, 5))
+    pre = [[]]
+    for h in range(1, len(lds)):
+        prev = pre[-1] if h > 1 else list(range(256))
+        cur = sorted(int(p) << 8 | int(x) for p, x in
+                     zip(rng.choice(prev, 3000), rng.integers(0, 256, 3000)))
+        cur.append(alpha >> (48 - lds[h - 1]))
+        cur = sorted(cur)
+        if h == 5:
+            cur = cur + cur[:40]  # unsorted (and duplicated) at this level
+        pre.append(cur if h > 1 else list(range(256)))
+    for key in keys:
+        runs = {}
+        for mode in (0, 2):
+            prev_mode = L.dpf_amd_set_prefix_expand(mode)
+            try:
+                ctx = dpf.create_evaluation_context(key)
+                outs, wires = [], []
+                for h in range(len(lds)):
+                    if h == 4:  # continue from a copy through the wire format
+                        ctx = dpf.parse_evaluation_context(ctx.serialize())
+                    outs.append(dpf.evaluate_until(h, pre[h] if h else [], ctx, raw=True))
+                    wires.append(ctx.serialize())
+                runs[mode] = (outs, wires)
+            finally:
+                L.dpf_amd_set_prefix_expand(prev_mode)
+        for h in range(len(lds)):
+            assert np.array_equal(runs[0][0][h], runs[2][0][h]), h
+            assert runs[0][1][h] == runs[2][1][h], h
+    # the reference's errors from the device path's fallback
+    for mode in (0, 2):
+        prev_mode = L.dpf_amd_set_prefix_expand(mode)
+        try:
+            ctx = dpf.create_evaluation_context(keys[0])
+            dpf.evaluate_until(0, [], ctx)
+            dpf.evaluate_until(1, [1, 2, 3], ctx)
+            with pytest.raises(DpfAmdError) as e:
+                dpf.evaluate_until(2, [(1 << 16) + 5], ctx)
+            assert e.value.code == 3
+            assert "out of range for hierarchy level 1" in str(e.value)
+            with pytest.raises(DpfAmdError) as e:
+                dpf.evaluate_until(2, [(7 << 8) | 1], ctx)
+            assert e.value.code == 3
+            assert "Prefix not present in ctx.partial_evaluations at hierarchy level 1" in \
+                str(e.value)
+        finally:
+            L.dpf_amd_set_prefix_expand(prev_mode)
