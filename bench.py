@@ -304,12 +304,18 @@ def bench_pir(args, world, rank, device):
     barrier(world)
     mq_ms = max_over_ranks(ev[0].elapsed_time(ev[1]) / args.steps, world)
     del mws, msel, mout, ws, sel
-    hr = None
+    hr = shard = None
     if world == 1 and not args.skip_handle_request:
         torch.cuda.empty_cache()
         hr = bench_handle_request(args, n, rec, db, device)
+        # one rank's share at N = 8 as a database of its own (2^23 records of
+        # c4): the whole request on the shard, the per-GPU time of a node
+        if n >= 8 * 128:
+            torch.cuda.empty_cache()
+            shard = (n // 8, bench_handle_request(args, n // 8, rec, db[:(n // 8) * rec], device,
+                                                  queries=(1, 8)))
     return dict(ok=ok, wall_s=wall, scan_ms=scan_ms, db_bytes=n * rec, per_gpu_bytes=per * rec,
-                records=n, mq=mq, mq_ms=mq_ms, hr=hr)
+                records=n, mq=mq, mq_ms=mq_ms, hr=hr, shard=shard)
 
 
 def bench_handle_request(args, n, rec, db_tensor, device, shard_devices=None,
@@ -806,6 +812,14 @@ def main(argv=None):
                     "ms_per_request": {str(q): v for q, v in hr.items()},
                     "db_GBps_at_q1": pir["db_bytes"] / (hr[1] / 1e3) / 1e9 if 1 in hr else None,
                     "correct": hr_ok}
+            if pir.get("shard"):
+                sn, (shr, sok) = pir["shard"]
+                out["pir"]["handle_request_one_eighth"] = {
+                    "what": "the same API on a database of %d records (c4 / 8: one rank's row "
+                            "shard at N = 8), one GPU" % sn,
+                    "ms_per_request": {str(q): v for q, v in shr.items()},
+                    "shard_GBps_at_q1": sn * 256 / (shr[1] / 1e3) / 1e9,
+                    "correct": sok}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -1305,7 +1305,16 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
   }
   uint128* seeds = sc.seeds;
   uint8_t* cbs = sc.cbs;
-  if (ctx.partial_evaluations_size() > 0 && start_level <= stop_level) {
+  // A list the device path left in HBM (this device) is looked up there by
+  // binary search (LookupPartialEvaluations), not read back to the host.
+  const ContextDeviceState* dstate = ctx.device_state().get();
+  int cur_dev = 0;
+  DPF_RETURN_IF_ERROR(HipStatus(hipGetDevice(&cur_dev), "hipGetDevice"));
+  const bool dev_lookup = dstate != nullptr && dstate->device() == cur_dev &&
+                          dstate->count() > 0 && start_level <= stop_level && n > 0;
+  if (dev_lookup) {
+    // the seeds and control bits come from the lookup kernel below
+  } else if (ctx.partial_evaluations_size() > 0 && start_level <= stop_level) {
     const int shift = stop_level - start_level;
     const auto& pes = ctx.partial_evaluations();
     const int64_t m = static_cast<int64_t>(pes.size());
@@ -1420,25 +1429,30 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
   CwArrays cw = KeyCws(ctx.key(), start_level, stop_level);
   const bool walk = levels > 0 && n > 0;
   using Part = UploadRing::HostPart;
-  // correction words through the upload ring; the pinned seeds / control
-  // bits (and pinned prefixes) by direct DMA
-  const Part cw_parts[3] = {{cw.seeds.data(), walk ? size_t(16) * levels : 0},
+  // correction words (and the lookup's count) through the upload ring; the
+  // pinned seeds / control bits (and pinned prefixes) by direct DMA
+  const int64_t count_n = n;
+  const Part cw_parts[4] = {{cw.seeds.data(), walk ? size_t(16) * levels : 0},
                             {cw.ccl.data(), walk ? size_t(levels) : 0},
-                            {cw.ccr.data(), walk ? size_t(levels) : 0}};
-  size_t cw_off[3];
-  const size_t cw_bytes = UploadRing::PackedLayout(cw_parts, 3, cw_off);
-  const Part parts[3] = {{seeds, size_t(16) * n},
-                         {cbs, size_t(n)},
-                         {prefixes.data(), walk ? size_t(16) * n : 0}};
-  size_t off[6];
-  const size_t bytes = cw_bytes + UploadRing::PackedLayout(parts, 3, off);
+                            {cw.ccr.data(), walk ? size_t(levels) : 0},
+                            {&count_n, dev_lookup ? sizeof(int64_t) : 0}};
+  size_t cw_off[4];
+  const size_t cw_bytes = UploadRing::PackedLayout(cw_parts, 4, cw_off);
+  const Part parts[3] = {{seeds, dev_lookup ? 0 : size_t(16) * n},
+                         {cbs, dev_lookup ? 0 : size_t(n)},
+                         {prefixes.data(), walk || dev_lookup ? size_t(16) * n : 0}};
+  const size_t seeds_bytes[2] = {size_t(16) * n, size_t(n)};
+  size_t off[7];
+  Part laid[3] = {{seeds, seeds_bytes[0]}, {cbs, seeds_bytes[1]}, parts[2]};
+  const size_t bytes = cw_bytes + UploadRing::PackedLayout(laid, 3, off) + 16;
   for (int i = 0; i < 3; ++i) {
     off[i] += cw_bytes;
     off[3 + i] = cw_off[i];
   }
+  off[6] = bytes - 16;  // the lookup's flags
   DPF_RETURN_IF_ERROR(buf->Alloc(bytes, s));
   char* d = buf->as<char>();
-  DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, cw_parts, 3, cw_bytes, cw_off, s));
+  DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, cw_parts, 4, cw_bytes, cw_off, s));
   for (int i = 0; i < 3; ++i) {
     if (parts[i].bytes == 0) continue;
     if (i < 2 || prefixes_pinned)
@@ -1450,6 +1464,25 @@ Status ComputePartialEvaluations(const DpfState& st, Span<const uint128> prefixe
   }
   *seeds_dev = d + off[0];
   *cb_dev = reinterpret_cast<uint8_t*>(d + off[1]);
+  if (dev_lookup) {
+    int* flags = reinterpret_cast<int*>(d + off[6]);
+    DPF_RETURN_IF_ERROR(HipStatus(hipMemsetAsync(flags, 0, sizeof(int), s), "hipMemsetAsync"));
+    const uint64_t root[2] = {ctx.key().seed().low(), ctx.key().seed().high()};
+    DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd::LookupPartialEvaluations(
+        d + off[2], reinterpret_cast<const int64_t*>(d + cw_off[3]), n,
+        stop_level - start_level, dstate->prefixes(), dstate->count(), dstate->seeds(),
+        dstate->cbs(), root, ctx.key().party() != 0, false, d + off[0],
+        reinterpret_cast<uint8_t*>(d + off[1]), flags, s)));
+    // the reference reports a missing prefix before it changes the context
+    int host_flags = 0;
+    DPF_RETURN_IF_ERROR(HipStatus(
+        hipMemcpyAsync(&host_flags, flags, sizeof(int), hipMemcpyDeviceToHost, s), "d2h"));
+    DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+    if (host_flags != 0)
+      return InvalidArgumentError(
+          "Prefix not present in ctx.partial_evaluations at hierarchy level " +
+          std::to_string(hierarchy_level));
+  }
   if (walk) {
     DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_seeds(
         n, levels, levels, d + off[0], *cb_dev, d + off[2], 0, d + off[3],
