@@ -147,6 +147,54 @@ static int SinglePointPartialEvaluation() {
   return 0;
 }
 
+// A context after EvaluateNext with prefixes (its list held on the device):
+// the reference's field accessors see the list, a copy sees the same list, a
+// serialize / parse round trip keeps it, and a parsed context (list on the
+// host) continues to the same outputs; writing the field takes it to the host.
+static int ContextListAccessors() {
+  std::vector<DpfParameters> ps(3);
+  ps[0].set_log_domain_size(8);
+  ps[1].set_log_domain_size(16);
+  ps[2].set_log_domain_size(24);
+  for (auto& p : ps) p.mutable_value_type()->mutable_integer()->set_bitsize(64);
+  auto dpf = DistributedPointFunction::CreateIncremental(ps);
+  CHECK_OK(dpf);
+  const uint128 alpha = 0xabcdef;
+  auto keys = (*dpf)->GenerateKeysIncremental(alpha, std::vector<uint128>{1, 2, 3});
+  CHECK_OK(keys);
+  auto ctx = (*dpf)->CreateEvaluationContext(keys->first);
+  CHECK_OK(ctx);
+  CHECK_OK((*dpf)->EvaluateNext<uint64_t>(Span<const uint128>(), *ctx));
+  std::vector<uint128> p1 = {3, 7, 8, 0xab, 0xab, 200};  // sorted, one duplicate
+  CHECK_OK((*dpf)->EvaluateNext<uint64_t>(p1, *ctx));
+  // tree indices of level 0 (8 bits, uint64: 2 elements per block): p >> 1
+  const std::vector<uint64_t> want = {1, 3, 4, 0x55, 100};
+  CHECK(ctx->partial_evaluations_size() == 5);
+  if (ctx->partial_evaluations_size() != 5) return 1;
+  for (int i = 0; i < 5; ++i)
+    CHECK(ctx->partial_evaluations(i).prefix().low() == want[i] &&
+          ctx->partial_evaluations(i).prefix().high() == 0);
+  EvaluationContext copy = *ctx;
+  CHECK(copy.partial_evaluations_size() == 5 &&
+        copy.partial_evaluations(4).seed().low() == ctx->partial_evaluations(4).seed().low());
+  EvaluationContext parsed;
+  CHECK(parsed.ParseFromString(ctx->SerializeAsString()));
+  CHECK(parsed.SerializeAsString() == ctx->SerializeAsString());
+  std::vector<uint128> p2 = {(uint128{0xab} << 8) | 0xcd, (uint128{0xab} << 8) | 0xef,
+                             (uint128{200} << 8) | 1};
+  auto a = (*dpf)->EvaluateNext<uint64_t>(p2, *ctx);
+  auto b = (*dpf)->EvaluateNext<uint64_t>(p2, parsed);
+  CHECK_OK(a);
+  CHECK_OK(b);
+  CHECK(*a == *b);
+  CHECK(ctx->SerializeAsString() == parsed.SerializeAsString());
+  // a write takes the (device-held) list of `copy` to the host first
+  copy.mutable_partial_evaluations(0)->set_control_bit(!copy.partial_evaluations(0).control_bit());
+  CHECK(copy.partial_evaluations_size() == 5 &&
+        copy.partial_evaluations(1).prefix().low() == want[1]);
+  return 0;
+}
+
 static int DcfGenEval() {
   DcfParameters p;
   p.mutable_parameters()->set_log_domain_size(5);
@@ -412,6 +460,7 @@ static int PirShardedPlainRequests() {
 
 int main() {
   if (FullDomainUint64() || IncrementalTuple() || SinglePointPartialEvaluation() ||
+      ContextListAccessors() ||
       DcfGenEval() || Registration() ||
       EvaluateAndApplyStops() || IncrementalManyPrefixes() || EvaluateAndApplyRepeatedKeys() ||
       PirShardedPlainRequests())
