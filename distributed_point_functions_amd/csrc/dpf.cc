@@ -1118,14 +1118,17 @@ class ContextDeviceState {
       std::vector<uint128> p(n), sd(n);
       std::vector<uint8_t> cb(n);
       dpf_internal_host::DeviceGuard g(device_);
-      if (n == 0 ||
-          hipMemcpy(p.data(), prefixes_, 16 * n, hipMemcpyDeviceToHost) != hipSuccess ||
+      host_.resize(n);  // the size partial_evaluations_size() reported, whatever happens
+      if (n == 0) return;
+      if (hipMemcpy(p.data(), prefixes_, 16 * n, hipMemcpyDeviceToHost) != hipSuccess ||
           hipMemcpy(sd.data(), seeds_, 16 * n, hipMemcpyDeviceToHost) != hipSuccess ||
           hipMemcpy(cb.data(), cbs_, n, hipMemcpyDeviceToHost) != hipSuccess) {
-        (void)hipGetLastError();
-        return;  // an unreadable list reads as empty: later lookups report it missing
+        // an accessor cannot return a status: the entries stay zero and the
+        // error goes to stderr
+        std::fprintf(stderr, "[dpf_amd] reading back a context's partial evaluations failed: %s\n",
+                     hipGetErrorString(hipGetLastError()));
+        return;
       }
-      host_.resize(n);
       for (size_t i = 0; i < n; ++i) {
         PartialEvaluation& x = host_[i];
         x.mutable_prefix()->set_high(Uint128High64(p[i]));
