@@ -427,9 +427,11 @@ int LaunchExpand(int, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
 #endif
 constexpr int kCoopBlock = DPF_COOP_BLOCK;
 #ifndef DPF_COOP_QUAD_BFS
-#define DPF_COOP_QUAD_BFS 2  // breadth-first levels run as quad steps (0-2; 2: c1 span 38.9 -> 36.5 us)
+// breadth-first levels run as quad steps (0-3; 2: c1 span 38.9 -> 36.5 us;
+// 3: the 512-child level as quads expanding both children of a parent)
+#define DPF_COOP_QUAD_BFS 3
 #endif
-static_assert(DPF_COOP_QUAD_BFS >= 0 && DPF_COOP_QUAD_BFS <= 2, "quad BFS levels: 0-2");
+static_assert(DPF_COOP_QUAD_BFS >= 0 && DPF_COOP_QUAD_BFS <= 3, "quad BFS levels: 0-3");
 
 // Phase timestamps of KExpandCoop (diagnostic builds only: tools/coop_trace.py
 // builds one translation unit with DPF_COOP_TRACE=1): per block, thread 0's
@@ -524,7 +526,7 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
     const uint32_t* cw_words = reinterpret_cast<const uint32_t*>(a.cw_seed);
     uint32_t* nw = reinterpret_cast<uint32_t*>(nodes);
 #pragma unroll
-    for (int j = 0; j < DPF_COOP_QUAD_BFS; ++j) {
+    for (int j = 0; j < (DPF_COOP_QUAD_BFS < 2 ? DPF_COOP_QUAD_BFS : 2); ++j) {
       const bool active = wave < (8 << j);  // 128 << j quads, 16 per wave
       uint32_t xq = 0u, tq = 0u;
       if (active) {
@@ -539,6 +541,25 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
       if (active) nw[qd * 4 + c] = c == 0 ? (xq | tq) : xq;
       __syncthreads();
     }
+#if DPF_COOP_QUAD_BFS > 2
+    {
+      // 512 children: quad qd (all 256 of them) expands parent qd into
+      // children 2qd and 2qd + 1 — two independent quad chains per lane
+      // instead of one lane-AES per child (latency-bound at 8 waves per CU)
+      const uint32_t w = nw[qd * 4 + c];
+      const uint32_t tp = QuadPerm<kQuadBcast<0>>(w) & 1u;
+      uint32_t x0 = c == 0 ? (w & ~1u) : w, x1 = x0, t0 = tp, t1 = tp;
+      const int64_t ci = cw0 + s + 6 + 2;
+      const uint32_t cwc = cw_words[ci * 4 + c];
+      const uint32_t cl = a.ccl[ci], cr = a.ccr[ci];
+      QuadWalkStep(x0, t0, 0u, cwc, cl, cr, c, kl, kd, L);
+      QuadWalkStep(x1, t1, 1u, cwc, cl, cr, c, kl, kd, L);
+      __syncthreads();  // every parent has been read
+      nw[(2 * qd) * 4 + c] = c == 0 ? (x0 | t0) : x0;
+      nw[(2 * qd + 1) * 4 + c] = c == 0 ? (x1 | t1) : x1;
+      __syncthreads();
+    }
+#endif
   }
 #endif
   uint32_t x[4] = {0u, 0u, 0u, 0u}, t = 0;
