@@ -110,6 +110,7 @@ def lib():
     _sig(L, "dpf_amd_inner_product", I32, P, I64, I64, P, I64, I32, P, P, P)
     _sig(L, "dpf_amd_xor_fold", I32, P, I32, I64, P, P)
     _sig(L, "dpf_amd_set_expand_depth", I32, I32)
+    _sig(L, "dpf_amd_set_expand_roots", I32, I32)
     _sig(L, "dpf_amd_set_scan_m4", I32, I32)
     _sig(L, "dpf_amd_set_walk_mode", I32, I32)
     _sig(L, "dpf_amd_set_dcf_kernel", I32, I32)

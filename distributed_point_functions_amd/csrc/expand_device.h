@@ -333,12 +333,20 @@ __global__ __launch_bounds__(kBlockOf<Em>, kWavesOf<Em>) void KExpand(ExpandArgs
     const int64_t cid = live ? id : total - 1;
     const int64_t key = kBatched ? cid / cpk : 0;
     const int64_t c = a.chunk_begin + (kBatched ? cid - key * cpk : cid);
-    const int64_t root = kBatched ? key : c >> a.walk;
-    const int64_t cw0 = kBatched ? key * a.num_levels : 0;
+    const int64_t root = kBatched ? key : (c >> a.walk) - a.root_base;
+    // first correction word of the walk: [key][level] when batched, else the
+    // level of the precomputed roots (0: the key's root)
+    const int64_t cw0 = kBatched ? key * a.num_levels : a.root_level;
     const uint64_t path = (uint64_t)c & ((a.walk >= 63) ? ~0ull : ((1ull << a.walk) - 1));
     uint4 s = a.root_seeds[root];
     uint32_t x[4] = {s.x, s.y, s.z, s.w};
-    uint32_t t = a.root_cb[root];
+    uint32_t t;
+    if (!kBatched && a.root_cb == nullptr) {  // packed node: control bit in the LSB
+      t = x[0] & 1u;
+      x[0] &= ~1u;
+    } else {
+      t = a.root_cb[root];
+    }
     for (int i = 0; i < a.walk; ++i) {
       const uint32_t bit = (uint32_t)(path >> (a.walk - 1 - i)) & 1u;
       const Cw cw = LoadCw(a.cw_seed, a.ccl, a.ccr, cw0 + i);
@@ -374,7 +382,7 @@ __global__ __launch_bounds__(kBlockOf<Em>, kWavesOf<Em>) void KExpand(ExpandArgs
       E.cw0 = cw0;
     }
     LeafStage S;
-    if (live) Dfs<D, D, Em>(E, S, x, t, a.walk, c, 0);
+    if (live) Dfs<D, D, Em>(E, S, x, t, kBatched ? a.walk : a.root_level + a.walk, c, 0);
   }
 }
 
@@ -460,6 +468,20 @@ extern "C" __attribute__((visibility("default"))) int dpf_amd_debug_coop_trace(v
 #endif
 static_assert(kCoopBlock == 1024, "the BFS levels assume 1024 threads (64 -> 1024 nodes)");
 constexpr int kCoopLog = 10;  // log2 nodes after the BFS
+
+// Tree nodes instead of leaves: KExpandCoop<0, EmitNodes> stores node g of its
+// last level as one packed 16-byte word (control bit in the seed's LSB) at
+// out[g - leaf_begin] — the roots stage of a large expansion
+// (dpf_amd_expand_and_correct), which KExpand then starts from.
+struct EmitNodes {
+  static constexpr int kBN = 1;
+  static constexpr bool kCanStage = false;
+  static constexpr bool kCanBatch = false;
+};
+template <class Em>
+inline constexpr bool kNodesEm = false;
+template <>
+inline constexpr bool kNodesEm<EmitNodes> = true;
 
 template <int E, class Em, bool kBatched>
 __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(ExpandArgs a,
@@ -598,7 +620,13 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
     Ec.kparty = a.key_party[key];
   }
   const int64_t g0 = chunk << K;  // first tree leaf of the block (per key if batched)
-  if constexpr (E == 0) {
+  if constexpr (kNodesEm<Em>) {
+    static_assert(E == 0 && !kBatched, "nodes are stored from the 1024-node level");
+    const int64_t g = g0 + tid;
+    if (g >= a.leaf_begin && g < a.leaf_end)
+      reinterpret_cast<uint4*>(a.out)[g - a.leaf_begin] =
+          make_uint4((x[0] & ~1u) | t, x[1], x[2], x[3]);
+  } else if constexpr (E == 0) {
     uint32_t xs[1][4] = {{x[0], x[1], x[2], x[3]}};
     uint32_t h[1][BN][4];
     HashWords<1, BN, true>(xs, h, L);

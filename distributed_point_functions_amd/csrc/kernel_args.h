@@ -44,7 +44,13 @@ struct ExpandArgs {
   int64_t leaf_begin;
   int64_t leaf_end;
   int32_t walk;  // levels walked per thread before the DFS
-  int32_t pad;
+  // Non-batched KExpand with precomputed roots: root_seeds are the tree nodes
+  // root_level levels below the key's root (root_seeds[i] = node root_base +
+  // i of that level), so chunk c starts at root_seeds[(c >> walk) -
+  // root_base] and walks levels root_level .. root_level + walk - 1.
+  // root_cb == nullptr: the control bit is the seed's LSB (packed nodes).
+  int32_t root_level;
+  int64_t root_base;
   // Batched keys (KExpandCoop<.., true>): key k = blockIdx.x / (chunk_end -
   // chunk_begin) has root_seeds[k] / root_cb[k], correction words
   // [k * num_levels + level], value correction key_corr[k] (packed block of
@@ -171,6 +177,9 @@ inline int HipCheck(hipError_t e, const char* what) {
 inline int LaunchCheck(const char* what) { return HipCheck(hipGetLastError(), what); }
 
 
+// k_expand_nodes.hip: the 1024-node levels of blocks [chunk_begin, chunk_end)
+// as packed nodes (KExpandCoop<0, EmitNodes>).
+int LaunchExpandNodes(hipStream_t st, const ExpandArgs& a, const VtDev& vt);
 // k_expand_*.hip: fused expansion with DFS depth D in {0,1,2,4,8}.
 int LaunchExpandU32ModN64(int D, int grid, hipStream_t st, const ExpandArgs& a,
                           const VtDev& vt);

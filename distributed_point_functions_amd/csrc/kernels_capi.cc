@@ -25,6 +25,13 @@ namespace {
 // changes what another thread's launches pick.
 thread_local int t_expand_depth = 0;  // dpf_amd_set_expand_depth
 thread_local int t_walk_mode = 0;     // dpf_amd_set_walk_mode
+// dpf_amd_set_expand_roots: -1 automatic, 0 off, 1 whenever eligible.
+// DPF_AMD_EXPAND_ROOTS=0 starts every thread with it off (A/B runs).
+const int kExpandRootsDefault = [] {
+  const char* e = std::getenv("DPF_AMD_EXPAND_ROOTS");
+  return (e && std::atoi(e) == 0) ? 0 : -1;
+}();
+thread_local int t_expand_roots = kExpandRootsDefault;
 thread_local int t_dcf_generic = 0;   // dpf_amd_set_dcf_kernel
 // dpf_amd_set_scan_m4; the process default comes from DPF_AMD_SCAN_M4 (A/B runs)
 const int kScanM4Default = [] {
@@ -313,16 +320,56 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
   a.out = (char*)out;
   const int sub = D >= 0 ? D : 9 - D;  // log2 leaves per thread (KExpand) or per block (coop)
   a.walk = num_levels - sub;
-  a.pad = 0;
+  a.root_level = 0;
+  a.root_base = 0;
   a.chunk_begin = leaf_begin >> sub;
   a.chunk_end = (leaf_end + (1ll << sub) - 1) >> sub;
   a.leaf_begin = leaf_begin;
   a.leaf_end = leaf_end;
   a.num_levels = num_levels;
   a.num_keys = 1;
+  // Precomputed subtree roots (D = 8 launches of >= 2^28 leaves, c5): every
+  // KExpand thread used to walk `walk` levels from the key's root to its
+  // subtree root, one AES per level — 24 levels per 256 leaves at c5, 15 of
+  // its 615 T-table lookups per leaf.  The levels above the last six are
+  // instead computed once per node, by KExpandCoop<0, EmitNodes> (every node
+  // of level R = walk - 6 of the launch's range, breadth-first in LDS), and
+  // each thread walks only the six levels its wave's lanes differ in.
+  hipStream_t st = (hipStream_t)stream;
+  constexpr int kCoopLog0 = 10;  // KExpandCoop<0>: 1024 nodes per block
+  distributed_point_functions::dpf_internal_host::DeviceBuffer roots;
+  const int roots_mode = t_expand_roots;
+  if (D == 8 && (forced == 0 || forced == 8) && roots_mode != 0 && a.walk >= 6 + 11 &&
+      (roots_mode > 0 || range >= (int64_t{1} << 28))) {
+    const int R = a.walk - 6;
+    const int64_t rb = a.chunk_begin >> 6, re = ((a.chunk_end - 1) >> 6) + 1;
+    distributed_point_functions::Status ast = roots.Alloc(size_t(16) * (re - rb), st);
+    if (!ast.ok()) return SetError(ast.raw_code(), ast.message());
+    ExpandArgs r{};
+    r.root_seeds = a.root_seeds;
+    r.root_cb = a.root_cb;
+    r.cw_seed = a.cw_seed;
+    r.ccl = a.ccl;
+    r.ccr = a.ccr;
+    r.out = roots.as<char>();
+    r.walk = R - kCoopLog0;
+    r.chunk_begin = rb >> kCoopLog0;
+    r.chunk_end = (re + (int64_t{1} << kCoopLog0) - 1) >> kCoopLog0;
+    r.leaf_begin = rb;
+    r.leaf_end = re;
+    r.num_levels = R;
+    r.num_keys = 1;
+    rc = LaunchExpandNodes(st, r, dev);
+    if (rc != DPF_AMD_OK) return rc;
+    a.root_seeds = roots.as<const uint4>();
+    a.root_cb = nullptr;
+    a.root_base = rb;
+    a.root_level = R;
+    a.walk = 6;
+  }
   // LaunchExpand caps the grid (DPF_EXPAND_MAX_GRID).
   const int grid = GridFor(a.chunk_end - a.chunk_begin, kExpandBlock, INT32_MAX);
-  return LaunchExpandForType(D, grid, (hipStream_t)stream, a, dev);
+  return LaunchExpandForType(D, grid, st, a, dev);
 }
 
 int dpf_amd_expand_and_correct_batched(int64_t num_keys, const void* root_seeds,
@@ -381,6 +428,13 @@ int dpf_amd_set_expand_depth(int depth) {
     return -3;
   const int old = t_expand_depth;
   t_expand_depth = depth;
+  return old;
+}
+
+int dpf_amd_set_expand_roots(int mode) {
+  if (mode < -1 || mode > 1) return -2;
+  const int old = t_expand_roots;
+  t_expand_roots = mode;
   return old;
 }
 

@@ -143,6 +143,24 @@ class forced_expand_depth:
         _lib.lib().dpf_amd_set_expand_depth(self.prev)
 
 
+class forced_expand_roots:
+    """Context manager for the roots stage of large expansions
+    (dpf_amd_set_expand_roots: -1 automatic, 0 never, 1 whenever eligible)."""
+
+    def __init__(self, mode: int):
+        self.mode = mode
+
+    def __enter__(self):
+        prev = _lib.lib().dpf_amd_set_expand_roots(self.mode)
+        if prev < -1:
+            raise ValueError("expand roots mode must be -1, 0 or 1")
+        self.prev = prev
+        return self
+
+    def __exit__(self, *exc):
+        _lib.lib().dpf_amd_set_expand_roots(self.prev)
+
+
 class forced_scan_m4:
     """Context manager selecting dpf_amd_inner_product's scan kernel
     (dpf_amd_set_scan_m4: -1 automatic, 0 masked scan, 1 Four-Russians)."""

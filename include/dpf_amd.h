@@ -177,6 +177,17 @@ int dpf_amd_expand_and_correct_batched(
  * (setting unchanged). */
 int dpf_amd_set_expand_depth(int depth);
 
+/* Testing knob (calling thread only): the roots stage of large expansions.
+ * A KExpand<8> launch normally walks every thread from the key's root down to
+ * its 256-leaf subtree; with the roots stage the nodes six levels above the
+ * subtree roots are computed once, breadth-first (KExpandCoop), and each
+ * thread walks six levels from there.  -1 = automatic (launches of >= 2^28
+ * leaves at D = 8 with >= 17 levels above the subtrees), 0 = never, 1 =
+ * whenever the launch is eligible regardless of size (tests).  Every thread
+ * starts from -1, or 0 with DPF_AMD_EXPAND_ROOTS=0.  Returns the previous
+ * setting, or -2 for an invalid mode (unchanged). */
+int dpf_amd_set_expand_roots(int mode);
+
 /* Testing knob (calling thread only): which XOR scan dpf_amd_inner_product
  * runs on launches issued by this thread.
  * -1 automatic (the Four-Russians many-query scan from 16 queries on, records

@@ -86,6 +86,29 @@ def test_kernel_choice_hooks_are_per_thread():
     assert L.dpf_amd_set_scan_m4(-1) == 1
 
 
+def test_expand_roots_hook_validates_and_is_per_thread():
+    """dpf_amd_set_expand_roots: -1 / 0 / 1, -2 (unchanged) otherwise, per
+    thread (no GPU needed)."""
+    import threading
+    from distributed_point_functions_amd import _lib
+    L = _lib.lib()
+    start = -1 if os.environ.get("DPF_AMD_EXPAND_ROOTS") != "0" else 0
+    assert L.dpf_amd_set_expand_roots(2) == -2
+    assert L.dpf_amd_set_expand_roots(-2) == -2
+    assert L.dpf_amd_set_expand_roots(1) == start
+    seen = {}
+
+    def other():
+        seen["first"] = L.dpf_amd_set_expand_roots(0)
+        seen["back"] = L.dpf_amd_set_expand_roots(start)
+
+    t = threading.Thread(target=other)
+    t.start()
+    t.join()
+    assert seen == {"first": start, "back": 0}
+    assert L.dpf_amd_set_expand_roots(start) == 1
+
+
 def test_walk_and_dcf_kernel_hooks_validate_and_are_per_thread():
     """dpf_amd_set_walk_mode (0 / 1 / 2) and dpf_amd_set_dcf_kernel (0 / 1):
     invalid values are refused unchanged, and another thread keeps its own

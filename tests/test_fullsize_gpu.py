@@ -168,6 +168,47 @@ def test_automatic_cooperative_launch_matches_oracle(K, cuda, ld):
     torch.cuda.empty_cache()
 
 
+ROOTS = [(C5, 25), (("int", 64), 26), (("xor", 128), 25)]
+
+
+@pytest.mark.parametrize("spec,ld", ROOTS, ids=["%r-ld%d" % a for a in ROOTS])
+def test_roots_stage_matches_oracle(K, cuda, spec, ld):
+    """The roots stage of large KExpand<8> launches (kernels_capi.cc: the
+    nodes six levels above the 256-leaf subtrees computed once by
+    KExpandCoop<0, EmitNodes>, each thread walking six levels from there)
+    forced on 2^25-tree-leaf domains — the whole domain and ragged ranges that
+    start and end inside a subtree, a 64-subtree root group and a 1024-node
+    block of the roots stage — both parties against the oracle."""
+    import torch
+    d, k0, k1, alpha, beta = _keys(spec, ld, seed=23)
+    L = d.hierarchy_to_tree(0)
+    assert L - 8 >= 17
+    n = 1 << L
+    ranges = [(1, n - 1), (255, 257), ((64 << 8) - 1, (3 * 64 << 8) + 5),
+              ((1024 * 64 << 8) - 3, (1024 * 64 << 8) + 300), (12345, 12345 + (1 << 20) + 77),
+              (n - 300, n)]
+    with K.forced_expand_roots(1), K.forced_expand_depth(8):
+        for key in (k0, k1):
+            want = d.evaluate_until_words(0, [], d.create_evaluation_context(key))
+            got = _expand(K, cuda, d, key, spec).cpu().numpy()
+            _assert_host_layout_equals_words(spec, got, want, "ld %d party %d" % (ld, key.party))
+            del got
+            e = len(want) // n  # elements per tree leaf
+            for lo, hi in ranges:
+                got = _expand(K, cuda, d, key, spec, lo, hi).cpu().numpy()
+                _assert_host_layout_equals_words(spec, got, want[lo * e:hi * e],
+                                                 "party %d [%d, %d)" % (key.party, lo, hi))
+            del want
+    torch.cuda.empty_cache()
+
+
+def test_forced_expand_roots_knob_validates():
+    from distributed_point_functions_amd import kernels as K
+    with pytest.raises(ValueError):
+        with K.forced_expand_roots(2):
+            pass
+
+
 def test_forced_depth_knob_validates():
     from distributed_point_functions_amd import kernels as K
     with pytest.raises(ValueError):
