@@ -444,7 +444,7 @@ static_assert(DPF_COOP_QUAD_BFS >= 0 && DPF_COOP_QUAD_BFS <= 3, "quad BFS levels
 // Phase timestamps of KExpandCoop (diagnostic builds only: tools/coop_trace.py
 // builds one translation unit with DPF_COOP_TRACE=1): per block, thread 0's
 // s_memrealtime (100 MHz) at entry, after the tables, after the walk, after
-// the BFS and at the end.
+// the BFS and at the end (slots 0-4), after each quad BFS level (5-7).
 #if DPF_COOP_TRACE
 __device__ uint64_t g_coop_trace[4096 * 8];
 #define DPF_COOP_MARK(i)                                                      \
@@ -562,6 +562,7 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
       __syncthreads();  // every parent of this level has been read
       if (active) nw[qd * 4 + c] = c == 0 ? (xq | tq) : xq;
       __syncthreads();
+      DPF_COOP_MARK(5 + j);
     }
 #if DPF_COOP_QUAD_BFS > 2
     {
@@ -580,6 +581,7 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
       nw[(2 * qd) * 4 + c] = c == 0 ? (x0 | t0) : x0;
       nw[(2 * qd + 1) * 4 + c] = c == 0 ? (x1 | t1) : x1;
       __syncthreads();
+      DPF_COOP_MARK(7);
     }
 #endif
   }

@@ -66,6 +66,12 @@ def main():
            "start_spread_us": (t[:, 0].max() - t0) / 100.0}
     for i, n in enumerate(names):
         res[n + "_us"] = {"median": float(np.median(ph[:, i])), "max": float(ph[:, i].max())}
+    # quad BFS levels (slots 5-7: after the 128-, 256- and 512-child levels)
+    q = buf.reshape(4096, 8)[:blocks].astype(np.int64)
+    if (q[:, 5:8] > 0).all():
+        marks = [q[:, 2], q[:, 5], q[:, 6], q[:, 7], q[:, 3]]
+        for i, n in enumerate(["bfs128", "bfs256", "bfs512", "bfs1024"]):
+            res[n + "_us"] = float(np.median((marks[i + 1] - marks[i]) / 100.0))
     print(json.dumps(res), flush=True)
 
 
