@@ -609,18 +609,23 @@ class UploadRing {
   }
 
  private:
-  // DPF_AMD_UPLOAD = sdma (default: hipMemcpyAsync from the pinned slot) |
-  // sdma_sync | kernel | kernel_coherent (a copy kernel reading the mapped
-  // slot) — diagnostics of the H2D path.
+  // DPF_AMD_UPLOAD = kernel_coherent (default: a copy kernel on the
+  // caller's stream reading the slot, mapped as fine-grained uncached memory)
+  // | kernel (the slot mapped non-coherent) | sdma (hipMemcpyAsync from the
+  // slot) | sdma_sync.  The copy kernel needs no copy-engine hand-off before
+  // the consumer kernel: 64 C++ EvaluateAt calls 7.74-7.88 ms against
+  // 7.84-8.38 with sdma on one box, 7.72-7.86 against 8.29-8.35 on another
+  // (profiles/ab_upload_r05n.log; the other C++ configs and the c4/8 request
+  // within noise).
   enum UploadMode { kKernel, kKernelCoherent, kSdma, kSdmaSync };
   static UploadMode Mode() {
     static const UploadMode m = [] {
       const char* e = std::getenv("DPF_AMD_UPLOAD");
-      if (!e) return kSdma;
+      if (!e) return kKernelCoherent;
       if (!std::strcmp(e, "kernel")) return kKernel;
-      if (!std::strcmp(e, "kernel_coherent")) return kKernelCoherent;
+      if (!std::strcmp(e, "sdma")) return kSdma;
       if (!std::strcmp(e, "sdma_sync")) return kSdmaSync;
-      return kSdma;
+      return kKernelCoherent;
     }();
     return m;
   }

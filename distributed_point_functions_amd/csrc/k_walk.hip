@@ -263,15 +263,43 @@ __global__ __launch_bounds__(kPointsBlockOf<BN>, kPointsWavesOf<BN>) void KEvalu
 
 // T4: four 64 KiB-halved tables (aes_device.h FillTables4, 128 KiB per
 // block), for launches of at most kQuadT4MaxPoints points (one block per CU).
+#ifndef DPF_QUAD_AHEAD
+#define DPF_QUAD_AHEAD 1
+#endif
+// Phase timestamps of KEvaluatePointsQuad (diagnostic builds only,
+// DPF_QUAD_TRACE=1, tools/quad_trace.py): per block, thread 0's s_memtime
+// (shader clock) and s_memrealtime (100 MHz) at entry, after the tables,
+// after the walk and at the end.
+#if DPF_QUAD_TRACE
+__device__ uint64_t g_quad_trace[4096 * 8];
+#define DPF_QUAD_MARK(i)                                                     \
+  do {                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) {                             \
+      g_quad_trace[blockIdx.x * 8 + 2 * (i)] = __builtin_amdgcn_s_memtime();  \
+      g_quad_trace[blockIdx.x * 8 + 2 * (i) + 1] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                        \
+  } while (0)
+extern "C" __attribute__((visibility("default"))) int dpf_amd_debug_quad_trace(void* host,
+                                                                               int64_t bytes) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_quad_trace), (size_t)bytes, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#else
+#define DPF_QUAD_MARK(i) \
+  do {                   \
+  } while (0)
+#endif
 template <int BN, bool T4>
 __global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluatePointsQuad(PointsArgs a,
                                                                                    VtDev vt) {
   __shared__ uint32_t tab[T4 ? kTab4Words : kTabWords];
+  DPF_QUAD_MARK(0);
   if constexpr (T4)
     FillTables4(tab);
   else
     FillTables(tab);
   __syncthreads();
+  DPF_QUAD_MARK(1);
   using LT = std::conditional_t<T4, Lds4, Lds>;
   LT L;
   if constexpr (T4)
@@ -304,6 +332,35 @@ __global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluatePointsQua
       const uint64_t j = (uint64_t)(ppk > 0 ? i - src * ppk : i) + (uint64_t)w.path_offset;
       p = make_uint4((uint32_t)j, (uint32_t)(j >> 32), 0u, 0u);
     }
+#if DPF_QUAD_AHEAD
+    // A level is ~1,100 cycles of dependent rounds: its correction word and
+    // path bit are loaded / formed one level ahead, off the chain, and the
+    // path sits in a shift register whose top bit is the next level's bit
+    // (PathBit's uniform word choice compiled to a branch tree in the loop).
+    const int nl = w.num_levels;
+    const int top = nl + w.rightshift;  // path bits [rightshift, top) are walked, msb first
+    u128 pp = (u128)p.x | ((u128)p.y << 32) | ((u128)p.z << 64) | ((u128)p.w << 96);
+    if (top > 128)
+      pp >>= (top - 128);  // the levels above bit 127 walk zeros (PathBit)
+    else if (top > 0 && top < 128)
+      pp <<= (128 - top);
+    int64_t ci = cw_base;
+    uint32_t cw_n = nl > 0 ? cw_words[ci * 4 + c] : 0u;
+    uint32_t cl_n = nl > 0 ? w.ccl[ci] : 0u, cr_n = nl > 0 ? w.ccr[ci] : 0u;
+    for (int level = 0; level < nl; ++level) {
+      const uint32_t cwc = cw_n, cl = cl_n, cr = cr_n;
+      const uint32_t bit = (uint32_t)(pp >> 127);
+      pp <<= 1;
+      if (level + 1 < nl) ci += cw_step;
+      cw_n = cw_words[ci * 4 + c];
+      cl_n = w.ccl[ci];
+      cr_n = w.ccr[ci];
+      if constexpr (T4 || DPF_QUAD_RKM)
+        QuadWalkStepRk<T4>(x, t, bit, cwc, cl, cr, c, klr, kd, L);
+      else
+        QuadWalkStep(x, t, bit, cwc, cl, cr, c, kl, kd, L);
+    }
+#else
     for (int level = 0; level < w.num_levels; ++level) {
       const uint32_t bit = PathBit(p, w.num_levels - level - 1 + w.rightshift);
       const int64_t ci = cw_base + level * cw_step;
@@ -312,6 +369,8 @@ __global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluatePointsQua
       else
         QuadWalkStep(x, t, bit, cw_words[ci * 4 + c], w.ccl[ci], w.ccr[ci], c, kl, kd, L);
     }
+#endif
+    DPF_QUAD_MARK(2);
     if (w.seeds_out) {
       reinterpret_cast<uint32_t*>(w.seeds_out)[i * 4 + c] = x;
       if (c == 0) w.cb_out[i] = (uint8_t)t;
@@ -355,6 +414,7 @@ __global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluatePointsQua
     } else {
       EmitLeaf<BN>(vt, W, t != 0, party, vt.corr, bi, bi + 1, [dst](int) { return dst; });
     }
+    DPF_QUAD_MARK(3);
   }
 }
 
