@@ -10,6 +10,7 @@
 //   3  four lookups of the lane's own column, xor3 combine, no DPP
 //      (perm -> 4 ds_read -> xor3: the round without its cross-lane moves)
 //   4  mode 2 with one active lane
+//   5  AesQuad<true> (two tables, per-round masked key XOR: KExpandCoop's walk)
 // at 1, 4 and 8 waves per CU (one block per CU: 128 KiB of tables).
 // Not part of the library:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I distributed_point_functions_amd/csrc \
@@ -43,6 +44,9 @@ __global__ __launch_bounds__(512) void KQuadProbe(uint32_t* out, unsigned long l
   const Lds4 L = MakeLds4(tab);
   const int c = threadIdx.x & 3;
   const QuadRk k = MakeQuadRk<0>(c);
+  const QuadKey kl = MakeQuadKey<0>(c);
+  const QuadDiff kd = MakeQuadDiff(c);
+  const uint32_t m = 0u - ((threadIdx.x >> 2) & 1u);
   uint32_t w = (threadIdx.x * 0x9e3779b9u) ^ (blockIdx.x * 0x85ebca6bu);
   if (MODE == 4 && (threadIdx.x & 63) != 0) return;
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -53,6 +57,8 @@ __global__ __launch_bounds__(512) void KQuadProbe(uint32_t* out, unsigned long l
       w = AesQuadRk<true>(w, k, L);
     } else if constexpr (MODE == 1) {
       w = AesQuadRk<false>(w, k, LdsOf(L));
+    } else if constexpr (MODE == 5) {
+      w = AesQuad<true>(w, kl, kd, m, LdsOf(L));
     } else if constexpr (MODE == 2 || MODE == 4) {
 #pragma unroll
       for (int r = 0; r < 10; ++r) w ^= LoadT0(LdsOf(L), w, r & 3);
@@ -126,6 +132,7 @@ int main() {
     Run<2>("lds_chain", threads, iters);
     Run<3>("own_column_4_lookups", threads, iters);
     Run<4>("lds_chain_one_lane", threads, iters);
+    Run<5>("quad_masked_t2", threads, iters);
   }
   return 0;
 }
