@@ -42,11 +42,30 @@ def main(tag):
         for r in csv.DictReader(open(stats[0])):
             kstats[r["Name"]] = r
     pmc = collections.defaultdict(lambda: collections.defaultdict(list))
+    # per pass and kernel: (duration, counter, value) of every dispatch, so that
+    # a kernel launched at two sizes (the c4 scan and the c4/8 shard request
+    # both run KPirScanG<1,4>) also gets the counters of its largest launches
+    per_pass = collections.defaultdict(list)
     for f in sorted(glob.glob(os.path.join(src, "pmc_*", "*counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
             if "dpf_amd" not in r["Kernel_Name"]:
                 continue
             pmc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            per_pass[(f, r["Kernel_Name"])].append((dur, r["Counter_Name"], float(r["Counter_Value"])))
+    largest = collections.defaultdict(lambda: collections.defaultdict(list))
+    partial = set()
+    for (f, k), rows in per_pass.items():
+        top = max(d for d, _, _ in rows)
+        for d, c, v in rows:
+            if d >= top // 2:
+                largest[k][c].append(v)
+            else:
+                partial.add(k)
+    trace_dur = collections.defaultdict(list)
+    for tf in glob.glob(os.path.join(src, "trace", "*kernel_trace.csv")):
+        for r in csv.DictReader(open(tf)):
+            trace_dur[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     out = {}
     sha = os.path.join(src, "library.sha256")
     if os.path.exists(sha):
@@ -66,6 +85,21 @@ def main(tag):
             e["calls_in_trace"] = int(kstats[k]["Calls"])
         if "SQ_INSTS_VALU" in avg and "SQ_INSTS_LDS" in avg:
             e["lds_per_valu"] = avg["SQ_INSTS_LDS"] / max(avg["SQ_INSTS_VALU"], 1)
+        if k in partial:  # launches of several sizes: the largest ones alone too
+            la = {c: sum(v) / len(v) for c, v in largest[k].items()}
+            big = {"counters_per_launch": la, "launches": max(len(v) for v in largest[k].values())}
+            if "FETCH_SIZE" in la:
+                big["hbm_read_bytes"] = la["FETCH_SIZE"] * 1024 * 2
+            if "WRITE_SIZE" in la:
+                big["hbm_write_bytes"] = la["WRITE_SIZE"] * 1024
+            if "FETCH_SIZE" in la and "WRITE_SIZE" in la:
+                big["hbm_bytes"] = big["hbm_read_bytes"] + big["hbm_write_bytes"]
+            td = trace_dur.get(k, [])
+            if td:
+                tl = [d for d in td if d >= max(td) // 2]
+                big["avg_duration_ns"] = sum(tl) / len(tl)
+                big["calls_in_trace"] = len(tl)
+            e["largest_launches"] = big
         out[k] = e
     with open(os.path.join(dst, tag + "_pmc.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
@@ -82,6 +116,15 @@ def main(tag):
             e.get("hbm_read_bytes", 0) / 1e9, e.get("hbm_write_bytes", 0) / 1e9,
             c.get("SQ_INSTS_VALU", 0), c.get("SQ_INSTS_LDS", 0),
             c.get("SQ_LDS_BANK_CONFLICT", 0)))
+    multi = [(k, e["largest_launches"]) for k, e in kernels.items() if "largest_launches" in e]
+    if multi:
+        lines += ["", "Kernels launched at several sizes — their largest launches alone "
+                  "(dispatches of at least half the longest one's duration):", "",
+                  "| kernel | calls | avg ms | HBM read GB | HBM write GB |", "|---|---|---|---|---|"]
+        for k, b in multi:
+            lines.append("| `%s` | %s | %.3f | %.3f | %.3f |" % (
+                k[:90], b.get("calls_in_trace", "?"), b.get("avg_duration_ns", 0) / 1e6,
+                b.get("hbm_read_bytes", 0) / 1e9, b.get("hbm_write_bytes", 0) / 1e9))
     with open(os.path.join(dst, tag + "_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
