@@ -2090,16 +2090,27 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
     const int levels = m.tree_level;
     CwArrays cw = KeyCws(key, 0, levels);
     using Part = UploadRing::HostPart;
-    const Part parts[6] = {{tree, size_t(16) * n},
-                           {&seed, 16},
+    // The points (and element indices) stay in a pinned slot the kernel reads
+    // in place (zero-copy: each point's 16 bytes cross PCIe once, while the
+    // block fills its tables); the key's seed and correction words, read at
+    // every level, go to device memory.
+    const Part pts[2] = {{tree, size_t(16) * n}, {bidx, m.epb > 1 ? size_t(n) : 0}};
+    size_t poff[2];
+    const size_t pts_bytes = UploadRing::PackedLayout(pts, 2, poff);
+    bool staged = false;
+    int slot = -1;
+    const char* pdev = nullptr;
+    DPF_RETURN_IF_ERROR(ThreadUploadRing().Stage(pts, 2, pts_bytes, poff, &staged, &slot, &pdev));
+    const Part parts[6] = {{&seed, 16},
                            {cw.seeds.data(), size_t(16) * levels},
                            {cw.ccl.data(), size_t(levels)},
                            {cw.ccr.data(), size_t(levels)},
-                           {&cb, 1}};
+                           {&cb, 1},
+                           {staged ? nullptr : tree, staged ? 0 : size_t(16) * n}};
     size_t off[6];
     const size_t in_bytes = UploadRing::PackedLayout(parts, 6, off);
     const size_t bi_off = in_bytes;
-    const size_t out_off = bi_off + (m.epb > 1 ? ((size_t(n) + 15) & ~size_t{15}) : 0);
+    const size_t out_off = bi_off + (m.epb > 1 && !staged ? ((size_t(n) + 15) & ~size_t{15}) : 0);
     DeviceBuffer buf;
     trace.Mark("prepare");
     const size_t out_bytes = size_t(n) * vt.out_stride;
@@ -2110,23 +2121,37 @@ Status DistributedPointFunction::EvaluateAtRaw(const DpfKey& key, int hierarchy_
       DPF_RETURN_IF_ERROR(
           dpf_internal_host::ThreadRecycled<dpf_internal_host::PinnedOut>::Get().Get(
               out_bytes, &hout, &kout));
-    DPF_RETURN_IF_ERROR(buf.Alloc(out_off + (host_out ? 0 : out_bytes), s));
-    char* d = buf.as<char>();
-    if (!host_out) kout = d + out_off;
-    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 6, in_bytes, off, s));
-    if (m.epb > 1) DPF_RETURN_IF_ERROR(ThreadUploadRing().Copy(d + bi_off, bidx, n, s));
+    // with the points staged, the key's part is written by the host into
+    // fine-grained device memory (no copy kernel in front of the walk)
+    bool placed = false;
+    int pslot = -1;
+    char* pd = nullptr;
+    if (staged)
+      DPF_RETURN_IF_ERROR(ThreadUploadRing().Place(parts, 6, in_bytes, off, &placed, &pslot, &pd));
+    const size_t dev_bytes = (placed ? 0 : out_off) + (host_out ? 0 : out_bytes);
+    if (dev_bytes) DPF_RETURN_IF_ERROR(buf.Alloc(dev_bytes, s));
+    char* d = placed ? pd : buf.as<char>();
+    if (!host_out) kout = buf.as<char>() + (placed ? 0 : out_off);
+    if (!placed) DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 6, in_bytes, off, s));
+    if (m.epb > 1 && !staged) DPF_RETURN_IF_ERROR(ThreadUploadRing().Copy(d + bi_off, bidx, n, s));
     if (host_out) {
       if (dpf_internal_host::HasPadding(vt)) std::memset(hout, 0, out_bytes);
     } else {
       DPF_RETURN_IF_ERROR(ClearPadding(vt, kout, out_bytes, s));
     }
     trace.Mark("alloc+upload");
-    DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_points_batched(
-        1, n, d + off[1], reinterpret_cast<const uint8_t*>(d + off[5]), d + off[0], 0, levels,
-        d + off[2], reinterpret_cast<const uint8_t*>(d + off[3]),
-        reinterpret_cast<const uint8_t*>(d + off[4]), &vt,
-        m.epb > 1 ? reinterpret_cast<const uint8_t*>(d + bi_off) : nullptr, nullptr,
-        key.party(), nullptr, reinterpret_cast<const uint64_t*>(corr.data()), kout, s)));
+    const void* paths = staged ? pdev + poff[0] : d + off[5];
+    const uint8_t* bdev = m.epb > 1 ? reinterpret_cast<const uint8_t*>(
+                                          staged ? pdev + poff[1] : d + bi_off)
+                                    : nullptr;
+    const Status launched = AbiStatus(dpf_amd_evaluate_points_batched(
+        1, n, d + off[0], reinterpret_cast<const uint8_t*>(d + off[4]), paths, 0, levels,
+        d + off[1], reinterpret_cast<const uint8_t*>(d + off[2]),
+        reinterpret_cast<const uint8_t*>(d + off[3]), &vt, bdev, nullptr, key.party(), nullptr,
+        reinterpret_cast<const uint64_t*>(corr.data()), kout, s));
+    if (staged) DPF_RETURN_IF_ERROR(ThreadUploadRing().Release(slot, s));
+    if (placed) DPF_RETURN_IF_ERROR(ThreadUploadRing().ReleasePlaced(pslot, s));
+    DPF_RETURN_IF_ERROR(launched);
     trace.Mark("launch");
     if (host_out) {
       DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));

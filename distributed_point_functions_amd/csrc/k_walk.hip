@@ -294,6 +294,20 @@ __global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluatePointsQua
                                                                                    VtDev vt) {
   __shared__ uint32_t tab[T4 ? kTab4Words : kTabWords];
   DPF_QUAD_MARK(0);
+  // The lane's first point is read before the table fill: `paths` may be a
+  // pinned host slot mapped into the device (one EvaluateAt call's points,
+  // read in place), whose PCIe round trip then overlaps the fill.
+  const int64_t i_first = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+  uint4 p_first = make_uint4(0u, 0u, 0u, 0u);
+  uint32_t x_first = 0u, t_first = 0u;  // its seed word and control bit (no key index)
+  if (i_first < a.w.num_seeds) {
+    if (a.w.paths) p_first = a.w.paths[i_first];
+    if (a.w.key_index == nullptr) {
+      const int64_t si0 = a.w.points_per_key > 0 ? i_first / a.w.points_per_key : i_first;
+      x_first = reinterpret_cast<const uint32_t*>(a.w.seeds_in)[si0 * 4 + (threadIdx.x & 3)];
+      t_first = a.w.cb_in[si0];
+    }
+  }
   if constexpr (T4)
     FillTables4(tab);
   else
@@ -323,11 +337,12 @@ __global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluatePointsQua
     const int64_t src = w.key_index ? (int64_t)w.key_index[i] : ppk > 0 ? i / ppk : i;
     const int64_t cw_base = by_key ? src * w.num_levels : per_seed ? i : 0;
     const int64_t si = (ppk > 0 || (w.key_index && w.seeds_by_key)) ? src : i;
-    uint32_t x = reinterpret_cast<const uint32_t*>(w.seeds_in)[si * 4 + c];
-    uint32_t t = w.cb_in[si];
+    const bool first = i == i_first && w.key_index == nullptr;
+    uint32_t x = first ? x_first : reinterpret_cast<const uint32_t*>(w.seeds_in)[si * 4 + c];
+    uint32_t t = first ? t_first : w.cb_in[si];
     uint4 p;
     if (w.paths) {
-      p = w.paths[i];
+      p = i == i_first ? p_first : w.paths[i];
     } else {
       const uint64_t j = (uint64_t)(ppk > 0 ? i - src * ppk : i) + (uint64_t)w.path_offset;
       p = make_uint4((uint32_t)j, (uint32_t)(j >> 32), 0u, 0u);
