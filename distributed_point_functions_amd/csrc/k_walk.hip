@@ -390,6 +390,7 @@ __global__ __launch_bounds__(kPointsBlock, kPointsWaves) void KEvaluatePointsQua
       reinterpret_cast<uint32_t*>(w.seeds_out)[i * 4 + c] = x;
       if (c == 0) w.cb_out[i] = (uint8_t)t;
     }
+    if (a.out == nullptr) continue;  // a walk only (EvaluateSeeds): no value hash
     // value hash (HashExpandedSeeds, cc:523-547): blocks H_V(seed + j), a
     // 128-bit add (a walk of zero levels leaves the key's seed, bit 0 set or
     // not)
@@ -798,6 +799,23 @@ static void LaunchPointsQuad(int64_t n, hipStream_t st, const PointsArgs& a, con
 #ifndef DPF_WALK_QUAD_MAX
 #define DPF_WALK_QUAD_MAX (1 << 16)
 #endif
+
+// EvaluateSeeds with the DPF's own PRG keys (the kernel's built-in key
+// schedule).  A launch too small to fill the chip — the walk of a
+// heavy-hitters level's 2^16 unique prefixes, 8 levels each — runs four lanes
+// per seed (KEvaluatePointsQuad without the value hash) instead of a lone
+// lane's 16-lookup rounds; larger ones keep the generic kernel.
+int LaunchEvaluateSeedsDpf(int64_t n, hipStream_t st, const WalkArgs& a, const KeyPair& kp) {
+  const int mode = WalkMode();  // 0 automatic, 1 quad-lane, 2 one lane per seed
+  if (mode == 1 || (mode == 0 && n <= DPF_WALK_QUAD_MAX)) {
+    PointsArgs pa{};
+    pa.w = a;
+    pa.out = nullptr;
+    LaunchPointsQuad<1>(n, st, pa, VtDev{});
+    return LaunchCheck("evaluate_seeds kernel launch");
+  }
+  return LaunchEvaluateSeeds(n, st, a, kp);
+}
 
 int LaunchEvaluatePoints(int bn, int64_t n, hipStream_t st, const PointsArgs& a,
                          const VtDev& vt) {

@@ -193,6 +193,7 @@ int LaunchExpandGeneric2(int D, int grid, hipStream_t st, const ExpandArgs& a, c
 int LaunchExpandGeneric4(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt);
 // k_walk.hip
 int LaunchEvaluateSeeds(int64_t n, hipStream_t st, const WalkArgs& a, const KeyPair& kp);
+int LaunchEvaluateSeedsDpf(int64_t n, hipStream_t st, const WalkArgs& a, const KeyPair& kp);
 int LaunchEvaluatePoints(int bn, int64_t n, hipStream_t st, const PointsArgs& a,
                          const VtDev& vt);
 // The calling thread's point-walk kernel choice (dpf_amd_set_walk_mode).

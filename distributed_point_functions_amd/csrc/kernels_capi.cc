@@ -258,6 +258,9 @@ int dpf_amd_evaluate_seeds(int64_t num_seeds, int num_levels, int64_t num_correc
   a.num_levels = num_levels;
   a.rightshift = paths_rightshift;
   KeyPair kp = MakeKeyPair(key_left_lo, key_left_hi, key_right_lo, key_right_hi);
+  if (key_left_lo == kPrgKeyLeftLo && key_left_hi == kPrgKeyLeftHi &&
+      key_right_lo == kPrgKeyRightLo && key_right_hi == kPrgKeyRightHi)
+    return LaunchEvaluateSeedsDpf(num_seeds, (hipStream_t)stream, a, kp);
   return LaunchEvaluateSeeds(num_seeds, (hipStream_t)stream, a, kp);
 }
 

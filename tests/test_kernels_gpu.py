@@ -94,6 +94,42 @@ def test_evaluate_seeds_rightshift(K, cuda, rightshift):
     assert (K.tensor_u128(so), [int(x) for x in co.cpu().numpy()]) == want
 
 
+# The DPF's own PRG keys (distributed_point_function.cc:55-60): launches of up to 2^16 seeds with these keys run the
+# four-lanes-per-seed walk (KEvaluatePointsQuad without the value hash).
+@pytest.mark.parametrize("num_seeds", [1, 101, 1000, 1 << 16])
+@pytest.mark.parametrize("num_levels", [1, 8, 63, 128])
+@pytest.mark.parametrize("per_seed_cw", [False, True])
+@pytest.mark.parametrize("walk", [0, 1, 2], ids=["auto", "quad", "lane"])
+def test_evaluate_seeds_dpf_keys_every_walk(K, cuda, num_seeds, num_levels, per_seed_cw, walk):
+    if per_seed_cw and num_seeds * num_levels > 1 << 20:
+        pytest.skip("per-seed correction words of 2^16 seeds x 63+ levels: oracle time")
+    kl = (0x5be037ccf6a03de5 << 64) | 0x935f08d0a5b6a2fd
+    kr = (0xef94b6aedebb026c << 64) | 0xe2ea1fe0f66f4d0b
+    rng = np.random.default_rng(num_seeds * 131 + num_levels)
+    seeds = [int(a) << 64 | int(b) for a, b in rng.integers(0, 1 << 63, (num_seeds, 2))]
+    paths = [int(a) << 64 | int(b) for a, b in rng.integers(0, 1 << 63, (num_seeds, 2))]
+    cbs = [int(x) for x in rng.integers(0, 2, num_seeds)]
+    ncw = num_levels * num_seeds if per_seed_cw else num_levels
+    cws = [int(a) << 64 | int(b) for a, b in rng.integers(0, 1 << 63, (ncw, 2))]
+    ccl = [int(x) for x in rng.integers(0, 2, ncw)]
+    ccr = [int(x) for x in rng.integers(0, 2, ncw)]
+    for rs in (0, 3):
+        want = po.evaluate_seeds(seeds, cbs, paths, rs, cws, ccl, ccr, kl, kr, num_levels)
+        with K.forced_walk_mode(walk):
+            s_in = K.u128_tensor(seeds, cuda)
+            c_in = u8(cbs, cuda)
+            so, co = K.evaluate_seeds(s_in, c_in, K.u128_tensor(paths, cuda), rs,
+                                      K.u128_tensor(cws, cuda), u8(ccl, cuda), u8(ccr, cuda),
+                                      kl, kr, num_levels)
+            # in place, as the heavy-hitters level walks its prefixes
+            K.evaluate_seeds(s_in, c_in, K.u128_tensor(paths, cuda), rs,
+                             K.u128_tensor(cws, cuda), u8(ccl, cuda), u8(ccr, cuda), kl, kr,
+                             num_levels, seeds_out=s_in, control_bits_out=c_in)
+        got = (K.tensor_u128(so), [int(x) for x in co.cpu().numpy()])
+        assert got == want
+        assert (K.tensor_u128(s_in), [int(x) for x in c_in.cpu().numpy()]) == want
+
+
 def test_evaluate_seeds_rejects_bad_correction_word_count(K, cuda):
     from distributed_point_functions_amd._lib import DpfAmdError
     s = K.u128_tensor([1] * 1000, cuda)
