@@ -564,6 +564,53 @@ __global__ __launch_bounds__(kCoopBlock, DPF_COOP_WAVES) void KExpandCoop(Expand
       __syncthreads();
       DPF_COOP_MARK(5 + j);
     }
+    if constexpr (E == -2) {
+      static_assert(DPF_COOP_QUAD_BFS >= 2, "E = -2 ends on the second quad level");
+      // 256 leaves per block (launches too small to give every CU a
+      // 1024-leaf block): the 256-node level is the last; node qd is hashed
+      // on its quad with the value key (HashWords' blocks H_V(seed + j) as
+      // quad rounds, the 128-bit seed + j formed from the broadcast columns)
+      // and the quad's lane 0 converts, corrects and stores it.
+      static_assert(!kNodesEm<Em>, "nodes are stored from the 1024-node level");
+      const uint32_t w = nw[qd * 4 + c];
+      const uint32_t tq = QuadPerm<kQuadBcast<0>>(w) & 1u;
+      const uint32_t xq = c == 0 ? (w & ~1u) : w;
+      const QuadRk kvr = MakeQuadRk<2>(c);
+      uint32_t h[BN][4];
+#pragma unroll
+      for (int j = 0; j < BN; ++j) {
+        uint32_t in = xq;
+        if (j > 0) {
+          const u128 v = ((u128)QuadPerm<kQuadBcast<0>>(xq) |
+                          ((u128)QuadPerm<kQuadBcast<1>>(xq) << 32) |
+                          ((u128)QuadPerm<kQuadBcast<2>>(xq) << 64) |
+                          ((u128)QuadPerm<kQuadBcast<3>>(xq) << 96)) +
+                         (u128)j;
+          in = (uint32_t)(v >> (32 * c));
+        }
+        const uint32_t sg = SigmaQuad(in, c);
+        const uint32_t hv = AesQuadRk<false>(sg, kvr, L) ^ sg;
+        h[j][0] = QuadPerm<kQuadBcast<0>>(hv);
+        h[j][1] = QuadPerm<kQuadBcast<1>>(hv);
+        h[j][2] = QuadPerm<kQuadBcast<2>>(hv);
+        h[j][3] = QuadPerm<kQuadBcast<3>>(hv);
+      }
+      ExpandArgs ak = a;
+      if constexpr (kBatched) ak.out += key * a.key_out_stride;
+      ExpandCtx Ec{ak, vt, L};
+      if constexpr (kBatched) {
+        const uint4 kc = a.key_corr[key];
+        Ec.per_key = true;
+        Ec.kcorr[0] = kc.x;
+        Ec.kcorr[1] = kc.y;
+        Ec.kcorr[2] = kc.z;
+        Ec.kcorr[3] = kc.w;
+        Ec.kparty = a.key_party[key];
+      }
+      if (c == 0) Em::Emit(Ec, h, tq, (chunk << K) + qd);
+      DPF_COOP_MARK(4);
+      return;
+    }
 #if DPF_COOP_QUAD_BFS > 2
     {
       // 512 children: quad qd (all 256 of them) expands parent qd into
@@ -679,7 +726,7 @@ int LaunchExpandCoop(hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
   return LaunchCheck("expand kernel launch");
 }
 
-// D >= 0: KExpand with DFS depth D; D = -1 / -2: KExpandCoop with E = 0 / 1.
+// D >= 0: KExpand with DFS depth D; D = -1 / -2 / -3: KExpandCoop with E = 0 / 1 / -2.
 // D = 6 is instantiated only for the PIR selection type (16-byte direct
 // elements), where large batched selection expansions use it.
 template <class Em>
@@ -691,6 +738,7 @@ template <class Em>
 int LaunchExpandAnyD(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
   if (D == -1) return LaunchExpandCoop<0, Em>(st, a, vt);
   if (D == -2) return LaunchExpandCoop<1, Em>(st, a, vt);
+  if (D == -3) return LaunchExpandCoop<-2, Em>(st, a, vt);
   if constexpr (kHasDepth6<Em>) {
     if (D == 6) return LaunchExpand<6, Em>(grid, st, a, vt);
   }

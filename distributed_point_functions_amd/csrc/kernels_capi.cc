@@ -56,7 +56,16 @@ int GridFor(int64_t items, int block, int max_blocks) {
 // E = 1 0.108 ms against KExpand<4> 0.125; from 2^23 KExpand<4>'s
 // full-occupancy register DFS wins (0.358 vs 0.384 ms) until KExpand<8> at
 // 2^25.
-int CoopDepth(int64_t leaves) { return leaves >= (int64_t{1} << 19) ? -2 : -1; }
+// Round 5 (tools/expand_sweep.py, profiles/sweep_single_r05v.log): up to
+// 2^16 leaves 256-leaf blocks (E = -2: the 1024 and 512-node levels and the
+// one-lane hashes replaced by the value hash on quads) — 2^11 13.4 vs 18.2 us,
+// 2^16 17.4 vs 21.7 us (the c4/8 PIR selection); level at 2^17, behind above.
+int CoopDepth(int64_t leaves) {
+  return leaves >= (int64_t{1} << 19) ? -2 : leaves > (int64_t{1} << 16) ? -1 : -3;
+}
+// log2 leaves per thread (KExpand, D >= 0) or per block: D = -1 / -2 / -3 are
+// KExpandCoop with E = 0 / 1 / -2 (1024 / 2048 / 256 leaves per block).
+int CoopSub(int D) { return D >= 0 ? D : D == -3 ? 8 : 9 - D; }
 constexpr int64_t kCoopMaxLeaves = int64_t{1} << 22;
 
 // Kernel for a batched expansion of num_keys x range tree leaves
@@ -311,7 +320,7 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
   if (num_levels >= 11 && range < kCoopMaxLeaves) D = CoopDepth(range);
   const int forced = t_expand_depth;
   if (forced > 0 && forced <= num_levels) D = forced;
-  if (forced < 0 && num_levels >= 10 - forced - 1) D = forced;
+  if (forced < 0 && num_levels >= CoopSub(forced)) D = forced;
   D = ResolveDepth(D, dev);
   if (D > num_levels) D = num_levels >= 4 ? 4 : num_levels;
   ExpandArgs a{};
@@ -321,7 +330,7 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
   a.ccl = ccl;
   a.ccr = ccr;
   a.out = (char*)out;
-  const int sub = D >= 0 ? D : 9 - D;  // log2 leaves per thread (KExpand) or per block (coop)
+  const int sub = CoopSub(D);  // log2 leaves per thread (KExpand) or per block (coop)
   a.walk = num_levels - sub;
   a.root_level = 0;
   a.root_base = 0;
@@ -427,8 +436,8 @@ int dpf_amd_expand_and_correct_batched(int64_t num_keys, const void* root_seeds,
 
 int dpf_amd_set_expand_depth(int depth) {
   if (depth != 0 && depth != 1 && depth != 2 && depth != 4 && depth != 6 && depth != 8 &&
-      depth != -1 && depth != -2)
-    return -3;
+      depth != -1 && depth != -2 && depth != -3)
+    return -99;
   const int old = t_expand_depth;
   t_expand_depth = depth;
   return old;
@@ -654,7 +663,7 @@ int ExpandBatched(int64_t num_keys, const void* root_seeds, const uint8_t* root_
   if (forced < 0) D = forced;
   D = ResolveDepth(D, dev);
   if (D > num_levels) D = 4;
-  const int sub = D >= 0 ? D : 9 - D;
+  const int sub = CoopSub(D);
   ExpandArgs a{};
   a.root_seeds = (const uint4*)root_seeds;
   a.root_cb = root_cb;

@@ -170,11 +170,11 @@ int dpf_amd_expand_and_correct_batched(
 
 /* Testing knob (calling thread only): forces the register-DFS depth D of the
  * fused expansion kernel KExpand to 1, 2, 4 or 8 whenever num_levels >= D,
- * or the cooperative kernel KExpandCoop with 1024 (-1) or 2048 (-2) leaves
- * per block whenever num_levels >= 10 / 11, so the kernels that other launch
- * sizes select can be checked on small domains.  0 restores the automatic
- * choice.  Returns the previous setting, or -3 for an invalid value
- * (setting unchanged). */
+ * or the cooperative kernel KExpandCoop with 1024 (-1), 2048 (-2) or 256 (-3)
+ * leaves per block whenever num_levels >= 10 / 11 / 8, so the kernels that
+ * other launch sizes select can be checked on small domains.  0 restores the
+ * automatic choice.  Returns the previous setting, or -99 for an invalid
+ * value (setting unchanged). */
 int dpf_amd_set_expand_depth(int depth);
 
 /* Testing knob (calling thread only): the roots stage of large expansions.

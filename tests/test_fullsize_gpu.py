@@ -124,12 +124,13 @@ def test_forced_depth_leaf_ranges(K, cuda, depth):
             _assert_host_layout_equals_words(C5, got, want[lo:hi], "[%d, %d)" % (lo, hi))
 
 
-@pytest.mark.parametrize("coop", [-1, -2])
+@pytest.mark.parametrize("coop", [-1, -2, -3])
 @pytest.mark.parametrize("spec", TYPES, ids=[repr(t) for t in TYPES])
 def test_cooperative_kernel_matches_oracle(K, cuda, spec, coop):
     """KExpandCoop (1024 / 2048 leaves per block: wave-0 walk to 64
-    sub-roots, four LDS breadth-first levels, one leaf per thread) forced on
-    a 2^16-element domain of every value type, both parties."""
+    sub-roots, four LDS breadth-first levels, one leaf per thread; 256 leaves
+    per block: two quad levels and the value hash on quads) forced on a
+    2^16-element domain of every value type, both parties."""
     d, k0, k1, alpha, beta = _keys(spec, 16, seed=20 - coop)
     assert d.hierarchy_to_tree(0) >= 11
     with K.forced_expand_depth(coop):
@@ -139,9 +140,9 @@ def test_cooperative_kernel_matches_oracle(K, cuda, spec, coop):
             _assert_host_layout_equals_words(spec, got, want, "party %d" % key.party)
 
 
-@pytest.mark.parametrize("coop", [-1, -2])
+@pytest.mark.parametrize("coop", [-1, -2, -3])
 def test_cooperative_kernel_leaf_ranges(K, cuda, coop):
-    """Ragged leaf ranges inside and across the 2^10 / 2^11-leaf blocks."""
+    """Ragged leaf ranges inside and across the 2^10 / 2^11 / 2^8-leaf blocks."""
     d, k0, _, _, _ = _keys(C5, 15, seed=4)
     want = d.evaluate_until_words(0, [], d.create_evaluation_context(k0))
     n = 1 << d.hierarchy_to_tree(0)
@@ -419,7 +420,7 @@ def test_c5_eight_rank_split_reproduces_one_rank(K, cuda, c5_full):
         assert _chunked_equal(buf, full), world
 
 
-@pytest.mark.parametrize("variant", [0, 2, 4, 6, 8, -1, -2])
+@pytest.mark.parametrize("variant", [0, 2, 4, 6, 8, -1, -2, -3])
 @pytest.mark.parametrize("spec,ld", [(("xor", 128), 14), (("int", 64), 15), (("int", 32), 16),
                                      (("int", 8), 18), (C5, 13)])
 def test_batched_keys_match_oracle(K, cuda, spec, ld, variant):
