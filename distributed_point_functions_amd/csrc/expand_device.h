@@ -447,15 +447,23 @@ static_assert(DPF_COOP_QUAD_BFS >= 0 && DPF_COOP_QUAD_BFS <= 3, "quad BFS levels
 // the BFS and at the end (slots 0-4), after each quad BFS level (5-7).
 #if DPF_COOP_TRACE
 __device__ uint64_t g_coop_trace[4096 * 8];
+__device__ uint64_t g_coop_clock[4096 * 8];  // s_memtime (shader clock) at the same marks
 #define DPF_COOP_MARK(i)                                                      \
   do {                                                                        \
     if (DPF_COOP_TRACE_SYNC) __syncthreads();                                 \
-    if (threadIdx.x == 0 && blockIdx.x < 4096)                                \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) {                              \
       g_coop_trace[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();  \
+      g_coop_clock[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime();      \
+    }                                                                         \
   } while (0)
 extern "C" __attribute__((visibility("default"))) int dpf_amd_debug_coop_trace(void* host,
                                                                                int64_t bytes) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_coop_trace), (size_t)bytes, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+extern "C" __attribute__((visibility("default"))) int dpf_amd_debug_coop_clock(void* host,
+                                                                               int64_t bytes) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_coop_clock), (size_t)bytes, 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
 }
 #else

@@ -66,6 +66,14 @@ def main():
            "start_spread_us": (t[:, 0].max() - t0) / 100.0}
     for i, n in enumerate(names):
         res[n + "_us"] = {"median": float(np.median(ph[:, i])), "max": float(ph[:, i].max())}
+    # the shader clock the blocks ran at (s_memtime against s_memrealtime)
+    cf = lib.dpf_amd_debug_coop_clock
+    cf.restype = ctypes.c_int
+    cf.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    clk = np.zeros(4096 * 8, dtype=np.uint64)
+    if cf(clk.ctypes.data, clk.nbytes) == 0:
+        ck = clk.reshape(4096, 8)[:blocks, :5].astype(np.int64)
+        res["shader_mhz"] = float(np.median((ck[:, 4] - ck[:, 0]) / (t[:, 4] - t[:, 0]) * 100.0))
     # quad BFS levels (slots 5-7: after the 128-, 256- and 512-child levels)
     q = buf.reshape(4096, 8)[:blocks].astype(np.int64)
     if (q[:, 5:8] > 0).all():
