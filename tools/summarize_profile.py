@@ -31,9 +31,9 @@ def short(name):
     return name.split("(")[0] if "(" in name and "<" not in name.split("(")[0][-1:] else name[:80]
 
 
-def main(tag):
-    src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
-    dst = os.path.join(ROOT, "profiles")
+def main(tag, root=ROOT):
+    src = os.path.join(root, "gpurun_out", "prof_" + tag)
+    dst = os.path.join(root, "profiles")
     os.makedirs(dst, exist_ok=True)
     stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
     kstats = {}
