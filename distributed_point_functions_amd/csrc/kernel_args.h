@@ -161,9 +161,11 @@ constexpr int64_t kScanSlotMaxBytes = 2048;
 constexpr int kScanM4Block = 256;
 constexpr int kScanM4Waves = kScanM4Block / 64;
 // Queries from which a scan pass uses KPirScanM4 (records of >= 64 bytes).
-// c4 (2^26 x 256 B): Q = 8 masked 2.55 ms vs M4 3.15; Q = 16 3.31 vs 2.91.
+// c4 (2^26 x 256 B), round 5 (profiles/c4q_masked_vs_m4_r05.log): Q = 8
+// masked 2.60 ms vs M4 2.84; Q = 9 2.86 vs 2.64, 12 2.96 vs 2.66, 15 3.12 vs
+// 2.69 (round 2 had measured only Q = 8 and 16 and set the switch at 16).
 #ifndef DPF_AMD_SCAN_M4_MIN_Q
-#define DPF_AMD_SCAN_M4_MIN_Q 16
+#define DPF_AMD_SCAN_M4_MIN_Q 9
 #endif
 constexpr int kScanM4MinQueries = DPF_AMD_SCAN_M4_MIN_Q;
 

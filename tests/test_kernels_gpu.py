@@ -94,8 +94,9 @@ def test_evaluate_seeds_rightshift(K, cuda, rightshift):
     assert (K.tensor_u128(so), [int(x) for x in co.cpu().numpy()]) == want
 
 
-# The DPF's own PRG keys (distributed_point_function.cc:55-60): launches of up to 2^16 seeds with these keys run the
-# four-lanes-per-seed walk (KEvaluatePointsQuad without the value hash).
+# The DPF's own PRG keys (distributed_point_function.cc:55-60): launches of up
+# to 2^16 seeds with these keys run the four-lanes-per-seed walk
+# (KEvaluatePointsQuad without the value hash).
 @pytest.mark.parametrize("num_seeds", [1, 101, 1000, 1 << 16])
 @pytest.mark.parametrize("num_levels", [1, 8, 63, 128])
 @pytest.mark.parametrize("per_seed_cw", [False, True])
@@ -396,6 +397,8 @@ SCAN_CASES = [(1, 16, 1), (1000, 256, 1), (1000, 256, 3), (4096, 80, 8), (300, 1
               # narrow last slice (1104 B = 4 x 256 + 80), 100 queries
               (1000, 256, 17), (3001, 256, 32), (4097, 512, 33), (130, 256, 64),
               (2500, 768, 100), (2049, 1104, 40), (640, 240, 16), (385, 64, 9),
+              # 9-15 queries: the Four-Russians scan from 9 on (P = 4)
+              (3000, 256, 12), (2001, 1104, 15), (1500, 256, 10),
               # >= 64 scan blocks with a partial of <= 2 KiB: the masked scan
               # XORs block partials into 64 atomic fold slots (ragged last
               # tile, two 64-chunk slices at 1104 B, Q x 256 B = 2 KiB)
