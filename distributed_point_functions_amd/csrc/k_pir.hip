@@ -372,6 +372,9 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
 #ifndef DPF_SCAN_M4_XTILE
 #define DPF_SCAN_M4_XTILE 1
 #endif
+#ifndef DPF_SCAN_M4_SKIP_IDLE
+#define DPF_SCAN_M4_SKIP_IDLE 1  // P = 1: lanes without a query skip their row reads
+#endif
 
 // The buffer resource of one 128-record tile, based at the tile.  The record
 // offset goes in voffset, which the range check covers: the last, partial
@@ -574,7 +577,8 @@ template <int P>
 __device__ __forceinline__ void ScanM4Tile2(uint4 s, __amdgpu_buffer_rsrc_t rs,
                                             __amdgpu_buffer_rsrc_t rn, int voff, int rec_bytes,
                                             bool col_ok, uint32_t (&xq)[8 * M4DualPrefetch(P)],
-                                            uint32_t (&acc)[64 / P], uint32_t* t, int cpart) {
+                                            uint32_t (&acc)[64 / P], uint32_t* t, int cpart,
+                                            bool q_ok) {
   constexpr int CPL = 16 / P;
   constexpr int ROW = 17;
   constexpr int DPF = M4DualPrefetch(P);
@@ -600,6 +604,7 @@ __device__ __forceinline__ void ScanM4Tile2(uint4 s, __amdgpu_buffer_rsrc_t rs,
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // groups 2k and 2k + 1: low nibble for table A
+    if (P == 1 && DPF_SCAN_M4_SKIP_IDLE && !q_ok) return;  // an idle lane reads nothing
     const uint4* ra = reinterpret_cast<const uint4*>(t) + (sb & 15) * ROW + cpart * CPL;
     const uint4* rb = reinterpret_cast<const uint4*>(t) + (16 + (sb >> 4)) * ROW + cpart * CPL;
     constexpr int RB = CPL < DPF_SCAN_M4_DUAL_RB ? CPL : DPF_SCAN_M4_DUAL_RB;
@@ -657,6 +662,17 @@ __device__ __forceinline__ void M4LaneMap(int lane, int& ql, int& cpart) {
     const uint32_t g = in_b ? kGroupB : ~kGroupB;
     cpart = 2 * (lane >> 5) + (int)in_b;
     ql = __builtin_popcount(g & ((1u << m) - 1u));
+  } else if constexpr (P == 1 && DPF_SCAN_M4_SKIP_IDLE) {
+    // queries fill the four lane groups in order (16 per group), so a pass of
+    // up to 48 queries leaves a whole group idle — and its lanes, which skip
+    // their row reads, cost the LDS nothing (row reads of lanes without a
+    // query used to read row 0: Q = 33 took as long as Q = 64)
+    constexpr uint32_t kGroupB = 0xF00F0FF0u;
+    const int m = lane & 31;
+    const uint32_t in_b = (kGroupB >> m) & 1u;
+    const uint32_t g = in_b ? kGroupB : ~kGroupB;
+    ql = 16 * (2 * (lane >> 5) + (int)in_b) + __builtin_popcount(g & ((1u << m) - 1u));
+    cpart = 0;
   } else {
     ql = lane % QW;
     cpart = lane / QW;
@@ -717,7 +733,7 @@ void KPirScanM4(ScanArgs a) {
       const uint4 sn = (q_ok && more) ? a.sel[(int64_t)(a.q0 + q) * a.sel_blocks + next]
                                       : make_uint4(0, 0, 0, 0);
       if constexpr (DUAL)
-        ScanM4Tile2<P>(s, rs, rn, voff, rec_bytes, col_ok, xq, acc, t, cpart);
+        ScanM4Tile2<P>(s, rs, rn, voff, rec_bytes, col_ok, xq, acc, t, cpart, q_ok);
       else
         ScanM4Tile<P>(s, rs, rn, voff, rec_bytes, col_ok, xq, acc, t, lane, cpart);
       if (!more) break;
