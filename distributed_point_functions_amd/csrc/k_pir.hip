@@ -774,7 +774,7 @@ constexpr int kScanM4PairBlock = 128;
 
 __device__ __forceinline__ void ScanM4PairStep(const uint32_t (&x)[4], uint32_t sb, int buf,
                                                uint32_t* t0, const uint4* tab0,
-                                               uint32_t (&acc)[64]) {
+                                               uint32_t (&acc)[64], bool q_ok) {
   constexpr int ROW = 17;
   // this wave's table in buffer `buf` (M0 = its base; buffer 1 is 8704 B on)
   uint32_t* t = t0 + buf * (2 * 16 * ROW * 4);
@@ -784,6 +784,7 @@ __device__ __forceinline__ void ScanM4PairStep(const uint32_t (&x)[4], uint32_t 
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  if (DPF_SCAN_M4_SKIP_IDLE && !q_ok) return;  // an idle lane reads nothing
   const uint4* ra = tab0 + (2 * buf) * 16 * ROW + (sb & 15) * ROW;
   const uint4* rb = tab0 + (2 * buf + 1) * 16 * ROW + (sb >> 4) * ROW;
   constexpr int RB = DPF_SCAN_M4_PAIR_RB;
@@ -809,7 +810,9 @@ void KPirScanM4Pair(ScanArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t part = blockIdx.x;  // block-uniform: both waves take the barriers
-  const int q = wave * 64 + lane;
+  int ql, cpart;
+  M4LaneMap<1>(lane, ql, cpart);  // queries fill whole lane groups (idle groups skip reads)
+  const int q = wave * 64 + ql;
   const int dw_lo = blockIdx.y * 64;
   const int width = min(64, a.C * 4 - dw_lo);
   const bool col_ok = lane < width;
@@ -846,7 +849,8 @@ void KPirScanM4Pair(ScanArgs a) {
           x[i] = xq[i];
           xq[i] = M4Prefetch(rs, rn, voff, rec_bytes, col_ok, 8 * (k + 1) + 4 * wave + i);
         }
-        ScanM4PairStep(x, (SelWord(s, k >> 2) >> (8 * (k & 3))) & 255, k & 1, t, tab0, acc);
+        ScanM4PairStep(x, (SelWord(s, k >> 2) >> (8 * (k & 3))) & 255, k & 1, t, tab0, acc,
+                       q_ok);
       }
       if (!more) break;
       tile = next;

@@ -19,7 +19,7 @@ echo "tests: $(tail -1 gpurun_out/ab_sp_tests_${TAG}.log)" | tee $LOG
 for i in $(seq 1 $ROUNDS); do
   for v in "$@"; do
     if [ $v = main ]; then export DPF_AMD_LIB=; else export DPF_AMD_LIB=$PWD/$N/var_$v/libdpf_amd.so; fi
-    timeout -k 10 300 python -u tools/bench_configs.py --only c4q --c4q-queries 33,40,48,64,100 --no-ab \
+    timeout -k 10 300 python -u tools/bench_configs.py --only c4q --c4q-queries 40,64,80,100,112 --no-ab \
       > gpurun_out/ab_sp.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/ab_sp.log; exit 1; }
     tail -1 gpurun_out/ab_sp.log | python3 -c "
 import json,sys; d=json.loads(sys.stdin.read()); print('$v', {k: round(v,3) for k,v in d.items() if k.endswith('_ms')})" | tee -a $LOG
