@@ -2361,16 +2361,26 @@ Status DistributedPointFunction::ExpandLeavesOnDevice(const DpfKey& key, int64_t
                          {cw.ccr.data(), size_t(L)}};
   size_t off[5];
   const size_t bytes = UploadRing::PackedLayout(parts, 5, off);
+  // written by the host into fine-grained device memory where the device
+  // allows it (no copy kernel in front of the expansion), else one copy
+  bool placed = false;
+  int pslot = -1;
+  char* d = nullptr;
+  DPF_RETURN_IF_ERROR(ThreadUploadRing().Place(parts, 5, bytes, off, &placed, &pslot, &d));
   DeviceBuffer in;
-  DPF_RETURN_IF_ERROR(in.Alloc(bytes, s));
-  char* d = in.as<char>();
-  DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 5, bytes, off, s));
+  if (!placed) {
+    DPF_RETURN_IF_ERROR(in.Alloc(bytes, s));
+    d = in.as<char>();
+    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 5, bytes, off, s));
+  }
   const int cepb = 1 << (m.log_domain - L);
-  return AbiStatus(dpf_amd_expand_and_correct(
+  const Status launched = AbiStatus(dpf_amd_expand_and_correct(
       1, d + off[0], reinterpret_cast<const uint8_t*>(d + off[1]), L, d + off[2],
       reinterpret_cast<const uint8_t*>(d + off[3]), reinterpret_cast<const uint8_t*>(d + off[4]),
       &vt, reinterpret_cast<const uint64_t*>(corr.data()), key.party(), cepb, leaf_begin,
       leaf_end, out, s));
+  if (placed) DPF_RETURN_IF_ERROR(ThreadUploadRing().ReleasePlaced(pslot, s));
+  return launched;
 }
 
 
@@ -2467,14 +2477,25 @@ Status DistributedPointFunction::ExpandLeavesOnDeviceBatched(Span<const DpfKey* 
       host[off_party + k] = static_cast<char>(key.party());
     }
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ThreadStream();
+    // host-written into fine-grained device memory where allowed (as in
+    // ExpandLeavesOnDevice), else one upload
+    const UploadRing::HostPart part{host.data(), host.size()};
+    bool placed = false;
+    int pslot = -1;
+    char* d = nullptr;
+    DPF_RETURN_IF_ERROR(ThreadUploadRing().Place(&part, 1, host.size(), nullptr, &placed, &pslot, &d));
     DeviceBuffer dev;
-    DPF_RETURN_IF_ERROR(dev.Upload(host.data(), host.size(), s));
-    char* d = dev.as<char>();
-    return AbiStatus(dpf_amd::ExpandBatched(
+    if (!placed) {
+      DPF_RETURN_IF_ERROR(dev.Upload(host.data(), host.size(), s));
+      d = dev.as<char>();
+    }
+    const Status launched = AbiStatus(dpf_amd::ExpandBatched(
         q, d, reinterpret_cast<const uint8_t*>(d + off_cb), L, d + off_cw,
         reinterpret_cast<const uint8_t*>(d + off_ccl), reinterpret_cast<const uint8_t*>(d + off_ccr),
         &vt, d + off_corr, reinterpret_cast<const int8_t*>(d + off_party), cepb, leaf_begin,
         leaf_end, out, s));
+    if (placed) DPF_RETURN_IF_ERROR(ThreadUploadRing().ReleasePlaced(pslot, s));
+    return launched;
   }
   if (!walk) {
     for (int64_t i = 0; i < q; ++i)

@@ -371,6 +371,59 @@ class PinnedOut {
   size_t cap_ = 0;
 };
 
+// The masked scan's atomic fold slots, kept zeroed between requests per
+// (device, stream index): the fold that reads them writes them back to zero
+// (dpf_amd::XorFoldClear), so a request needs no memset — one dispatch and
+// its dependent gap, ~10 us of a 0.4 ms shard request — in front of its
+// selection expansion.  A buffer is dirty from Acquire until the caller
+// launches the clearing fold (MarkClean); a dirty one (a request that stopped
+// between its scan and its fold, a new or grown buffer) is zeroed whole by
+// the next Acquire.  DPF_AMD_FOLD_CLEAR=0 zeroes on every Acquire (A/B).  The
+// previous user has synchronized.
+class FoldSlots {
+ public:
+  FoldSlots() = default;
+  FoldSlots(const FoldSlots&) = delete;
+  FoldSlots& operator=(const FoldSlots&) = delete;
+  ~FoldSlots() {
+    for (auto& e : m_)
+      if (e.second.p) (void)hipFree(e.second.p);
+  }
+  struct Entry {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool clean = false;
+  };
+  // Zeroed slots of at least `bytes` on the current device, ordered on `s`.
+  Status Acquire(int device, int index, size_t bytes, hipStream_t s, char** p, Entry** entry) {
+    static const bool always_zero = [] {
+      const char* e = std::getenv("DPF_AMD_FOLD_CLEAR");
+      return e != nullptr && std::strcmp(e, "0") == 0;
+    }();
+    Entry& e = m_[{device, index}];
+    if (e.cap < bytes) {
+      if (e.p) (void)hipFree(e.p);  // idle: its last user synchronized
+      e.p = nullptr;
+      e.cap = 0;
+      size_t cap = 64u << 10;
+      while (cap < bytes) cap <<= 1;
+      DPF_RETURN_IF_ERROR(HipStatus(hipMalloc(&e.p, cap), "hipMalloc(fold slots)"));
+      e.cap = cap;
+      e.clean = false;
+    }
+    if (!e.clean || always_zero)
+      DPF_RETURN_IF_ERROR(HipStatus(hipMemsetAsync(e.p, 0, e.cap, s), "scan slots memset"));
+    e.clean = false;
+    *p = static_cast<char*>(e.p);
+    *entry = &e;
+    return OkStatus();
+  }
+  static void MarkClean(Entry* e) { e->clean = true; }
+
+ private:
+  std::map<std::pair<int, int>, Entry> m_;
+};
+
 // Device-to-host copy into pageable `dst`, complete on return.  A plain
 // hipMemcpy into pageable memory stages through the runtime's own small
 // pinned buffers one after the other; copies above 1 MiB here go through two

@@ -149,5 +149,8 @@ int ScanFoldParts(const ScanPlan& plan);
 int ScanPiece(const void* db, int64_t num_records, int64_t record_stride,
               const void* selections, int64_t selection_blocks, int num_queries,
               const ScanPlan& plan, void* partials, void* stream);
+// dpf_amd_xor_fold that leaves the parts zeroed (fold slots reused by the
+// next request without a memset).
+int XorFoldClear(void* parts, int num_parts, int64_t bytes, void* out, void* stream);
 
 }  // namespace dpf_amd

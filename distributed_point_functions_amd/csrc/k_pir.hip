@@ -116,8 +116,10 @@ int CopyFromMappedHost(void* dst, const void* mapped_src, size_t bytes, void* st
 // a 2048-part fold of a few hundred bytes costs microseconds, not a serial
 // chain of 2048 dependent loads.
 
+// `clear` (the parts, or nullptr): every word is written back as zero after
+// its one read, so atomic fold slots are left zeroed for the next scan.
 __global__ __launch_bounds__(256) void KXorFold(const uint4* parts, int num_parts,
-                                                int64_t words, uint4* out) {
+                                                int64_t words, uint4* out, uint4* clear) {
   __shared__ uint4 red[kFoldSlices][kFoldWords];
   const int w = threadIdx.x % kFoldWords;
   const int s = threadIdx.x / kFoldWords;
@@ -127,6 +129,7 @@ __global__ __launch_bounds__(256) void KXorFold(const uint4* parts, int num_part
 #pragma unroll 8
     for (int p = s; p < num_parts; p += kFoldSlices) {
       const uint4 v = parts[(int64_t)p * words + i];
+      if (clear) clear[(int64_t)p * words + i] = make_uint4(0, 0, 0, 0);
       acc.x ^= v.x;
       acc.y ^= v.y;
       acc.z ^= v.z;
@@ -914,8 +917,9 @@ int LaunchGatherRows(int grid, hipStream_t st, int64_t n, const int64_t* src_off
 }
 
 int LaunchXorFold(unsigned blocks, hipStream_t st, const uint4* parts, int num_parts,
-                  int64_t words, uint4* out) {
-  hipLaunchKernelGGL(KXorFold, dim3(blocks), dim3(256), 0, st, parts, num_parts, words, out);
+                  int64_t words, uint4* out, uint4* clear) {
+  hipLaunchKernelGGL(KXorFold, dim3(blocks), dim3(256), 0, st, parts, num_parts, words, out,
+                     clear);
   return LaunchCheck("xor fold kernel launch");
 }
 

@@ -211,7 +211,7 @@ int LaunchGatherRows(int grid, hipStream_t st, int64_t n, const int64_t* src_off
                      int64_t opp, int64_t stride, const char* in, char* out,
                      int64_t in_rows = INT64_MAX, int* err = nullptr);
 int LaunchXorFold(unsigned blocks, hipStream_t st, const uint4* parts, int num_parts,
-                  int64_t words, uint4* out);
+                  int64_t words, uint4* out, uint4* clear = nullptr);
 int LaunchXorFoldBytes(int grid, hipStream_t st, const uint8_t* parts, int num_parts,
                        int64_t bytes, uint8_t* out);
 int LaunchPirScan(int nq, dim3 grid, hipStream_t st, const ScanArgs& a);

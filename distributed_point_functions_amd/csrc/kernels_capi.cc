@@ -600,6 +600,21 @@ ScanPlan PlanScan(int64_t num_records, int64_t record_stride, int num_queries) {
 
 int ScanFoldParts(const ScanPlan& plan) { return plan.slots ? kScanSlots : plan.grid; }
 
+int XorFoldClear(void* parts, int num_parts, int64_t bytes, void* out, void* stream) {
+  if (num_parts <= 0 || bytes <= 0) return DPF_AMD_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (bytes % 16 == 0 && ((uintptr_t)parts % 16 == 0) && ((uintptr_t)out % 16 == 0)) {
+    const int64_t words = bytes / 16;
+    const int64_t blocks = (words + kFoldWords - 1) / kFoldWords;
+    if (blocks > INT32_MAX) return SetError(DPF_AMD_INVALID_ARGUMENT, "xor fold too large");
+    return LaunchXorFold((unsigned)blocks, st, (const uint4*)parts, num_parts, words,
+                         (uint4*)out, (uint4*)parts);
+  }
+  const int rc = dpf_amd_xor_fold(parts, num_parts, bytes, out, stream);
+  if (rc != DPF_AMD_OK) return rc;
+  return HipCheck(hipMemsetAsync(parts, 0, (size_t)num_parts * bytes, st), "fold slots clear");
+}
+
 int ScanPiece(const void* db, int64_t num_records, int64_t record_stride,
               const void* selections, int64_t selection_blocks, int num_queries,
               const ScanPlan& plan, void* partials, void* stream) {

@@ -315,10 +315,12 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
   };
   struct Group {
     int device = 0;
+    int stream_index = 0;
     int64_t b0 = 0, b1 = 0;
     std::vector<Piece> pieces;
     hipStream_t s = nullptr;
     bool slots = true;
+    dpf_internal_host::FoldSlots::Entry* slot_entry = nullptr;
     int fold_parts = 0;
     void* buf = nullptr;
     char* sel = nullptr;
@@ -337,7 +339,8 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
         g.device = sh.device;
         g.b0 = b0;
         g.b1 = b0;
-        g.s = dpf_internal_host::ThreadStreamOn(sh.device, next_index[sh.device]++);
+        g.stream_index = next_index[sh.device]++;
+        g.s = dpf_internal_host::ThreadStreamOn(sh.device, g.stream_index);
         w.push_back(g);
       }
       Group& g = w.back();
@@ -388,15 +391,19 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
       }
       g.fold_parts = static_cast<int>(ws_bytes / part_bytes);
     }
+    // atomic fold slots live in the thread's zeroed FoldSlots, per-block
+    // partials in the request's allocation
     const int64_t sel_bytes = align(16 * nb * num_queries);
-    const int64_t total = sel_bytes + align(std::max<int64_t>(16, ws_bytes)) + part_bytes;
+    const int64_t ws_own = g.slots ? 0 : align(std::max<int64_t>(16, ws_bytes));
+    const int64_t total = sel_bytes + ws_own + part_bytes;
     st = DevicePool::Get().Alloc(total, g.s, &g.buf);
     if (!st.ok()) break;
     g.sel = static_cast<char*>(g.buf);
     g.ws = g.sel + sel_bytes;
-    g.part = g.ws + align(std::max<int64_t>(16, ws_bytes));
+    g.part = g.ws + ws_own;
     if (g.slots)
-      st = HipStatus(hipMemsetAsync(g.ws, 0, ws_bytes, g.s), "scan slots memset");
+      st = dpf_internal_host::ThreadRecycled<dpf_internal_host::FoldSlots>::Get().Acquire(
+          g.device, g.stream_index, ws_bytes, g.s, &g.ws, &g.slot_entry);
     if (st.ok()) st = fill(g.pieces[0].sh, g.b0, g.b0 + nb, g.sel, g.s);
     for (size_t k = 0; k < g.pieces.size() && st.ok(); ++k) {
       const Piece& pc = g.pieces[k];
@@ -407,9 +414,15 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
                                         num_queries, pc.plan, g.ws + (g.slots ? 0 : pc.ws_off),
                                         g.s));
     }
-    if (st.ok())
-      st = AbiStatus(dpf_amd_xor_fold(g.ws, g.fold_parts, part_bytes,
-                                      G == 1 && kout ? kout : g.part, g.s));
+    if (st.ok()) {
+      void* fold_out = G == 1 && kout ? kout : g.part;
+      if (g.slots) {
+        st = AbiStatus(dpf_amd::XorFoldClear(g.ws, g.fold_parts, part_bytes, fold_out, g.s));
+        if (st.ok()) dpf_internal_host::FoldSlots::MarkClean(g.slot_entry);
+      } else {
+        st = AbiStatus(dpf_amd_xor_fold(g.ws, g.fold_parts, part_bytes, fold_out, g.s));
+      }
+    }
     if (st.ok() && G > 1) {
       st = HipStatus(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "hipEventCreate");
       if (st.ok()) st = HipStatus(hipEventRecord(g.done, g.s), "hipEventRecord");
