@@ -321,6 +321,25 @@ def test_pir_batched_equals_singles_and_concurrent(api):
     assert not errors and all(r == batched for r in results)
 
 
+def test_pir_fold_slots_reused_across_request_sizes(api):
+    """A database large enough for the masked scan's atomic fold slots: the
+    slots are kept zeroed by the fold between requests (FoldSlots), so a
+    sequence of requests of different sizes — different slot widths in the
+    same buffer — must each reconstruct exactly."""
+    _, _, P = api
+    n = 1 << 17
+    records, dpf = _pir_setup(api, n, 32, seed=11)
+    server0 = _plain_server(api, records)
+    rng = np.random.default_rng(11)
+    for q in (1, 8, 3, 1, 5, 8, 2):
+        idx = [int(i) for i in rng.integers(0, n, q)]
+        pairs = P.client_keys(dpf, n, idx)
+        r0 = P.parse_response(server0.handle_request(P.pir_request_plain([a for a, _ in pairs])))
+        r1 = P.parse_response(server0.handle_request(P.pir_request_plain([b for _, b in pairs])))
+        for i, a, b in zip(idx, r0, r1):
+            assert bytes(x ^ y for x, y in zip(a, b)) == records[i], (q, i)
+
+
 def test_pir_leader_helper_end_to_end_with_one_time_pad(api):
     _, _, P = api
     n = 3000
