@@ -1607,19 +1607,7 @@ Status EvaluateUntilOnDevice(const DpfState& st, int hierarchy_level,
   int* flags = reinterpret_cast<int*>(w + o_flags);
   DPF_RETURN_IF_ERROR(HipStatus(hipMemsetAsync(flags, 0, sizeof(int), s), "hipMemsetAsync"));
   DPF_RETURN_IF_ERROR(ThreadUploadRing().Copy(w + o_p, prefixes.data(), 16 * size_t(n), s));
-  // the correction words host-written into fine-grained device memory where
-  // the device allows it (one copy kernel and its dispatch gap fewer per
-  // level), else one packed copy; `drain` keeps an early return from reusing
-  // the slot under a running kernel
-  bool cw_placed = false;
-  int cw_slot = -1;
-  char* cwp = nullptr;
-  DPF_RETURN_IF_ERROR(
-      ThreadUploadRing().Place(parts, 9, cw_bytes, coff, &cw_placed, &cw_slot, &cwp));
-  if (!cw_placed) {
-    cwp = w + o_cw;
-    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(cwp, parts, 9, cw_bytes, coff, s));
-  }
+  DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(w + o_cw, parts, 9, cw_bytes, coff, s));
   trace.Mark("upload");
   const uint64_t limit[2] = {prev_ld < 64 ? (uint64_t{1} << prev_ld) : 0,
                              prev_ld >= 64 && prev_ld < 128 ? (uint64_t{1} << (prev_ld - 64)) : 0};
@@ -1639,25 +1627,24 @@ Status EvaluateUntilOnDevice(const DpfState& st, int hierarchy_level,
   if (walk_levels > 0)
     DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_seeds(
         n, walk_levels, walk_levels, next->seeds(), next->cbs(), next->prefixes(), 0,
-        cwp + coff[0], reinterpret_cast<const uint8_t*>(cwp + coff[1]),
-        reinterpret_cast<const uint8_t*>(cwp + coff[2]), dpf_amd::kPrgKeyLeftLo,
+        w + o_cw + coff[0], reinterpret_cast<const uint8_t*>(w + o_cw + coff[1]),
+        reinterpret_cast<const uint8_t*>(w + o_cw + coff[2]), dpf_amd::kPrgKeyLeftLo,
         dpf_amd::kPrgKeyLeftHi, dpf_amd::kPrgKeyRightLo, dpf_amd::kPrgKeyRightHi, next->seeds(),
         next->cbs(), s)));
   // each prefix's own node, then its subtree (as the host path's fused branch)
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd::PrefixRoots(
-      n, pidx, plow, bbits, n, next->seeds(), next->cbs(), cwp + coff[3],
-      reinterpret_cast<const uint8_t*>(cwp + coff[4]),
-      reinterpret_cast<const uint8_t*>(cwp + coff[5]), w + o_ps,
+      n, pidx, plow, bbits, n, next->seeds(), next->cbs(), w + o_cw + coff[3],
+      reinterpret_cast<const uint8_t*>(w + o_cw + coff[4]),
+      reinterpret_cast<const uint8_t*>(w + o_cw + coff[5]), w + o_ps,
       reinterpret_cast<uint8_t*>(w + o_pcb), s)));
   void* final_dev = out_on_device ? out : static_cast<void*>(w + o_out);
   DPF_RETURN_IF_ERROR(ClearPadding(vt, final_dev, total * stride, s));
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_expand_and_correct(
-      n, w + o_ps, reinterpret_cast<const uint8_t*>(w + o_pcb), down, cwp + coff[6],
-      reinterpret_cast<const uint8_t*>(cwp + coff[7]),
-      reinterpret_cast<const uint8_t*>(cwp + coff[8]), &vt,
+      n, w + o_ps, reinterpret_cast<const uint8_t*>(w + o_pcb), down, w + o_cw + coff[6],
+      reinterpret_cast<const uint8_t*>(w + o_cw + coff[7]),
+      reinterpret_cast<const uint8_t*>(w + o_cw + coff[8]), &vt,
       reinterpret_cast<const uint64_t*>(corr.data()), ctx.key().party(), cepb, 0, n << down,
       final_dev, s)));
-  if (cw_placed) DPF_RETURN_IF_ERROR(ThreadUploadRing().ReleasePlaced(cw_slot, s));
   DPF_RETURN_IF_ERROR(CopyToHost(readback, flags, sizeof(int), s));
   DPF_RETURN_IF_ERROR(CopyToHost(readback + 1, next->count_dev(), sizeof(int64_t), s));
   trace.Mark("launch");
