@@ -85,8 +85,9 @@ def launch_decision(args, env, device_count):
     N rank processes itself (--gpus N > 1 and no WORLD_SIZE), or ("error",
     message) when the request cannot be honoured: a world size that is not
     --gpus, or more RCCL ranks than visible GPUs.  --in-process and
-    --experiments drive their devices from this one process."""
-    if args.in_process or args.experiments:
+    --experiments / --library-multi-device drive their devices from this one
+    process."""
+    if args.in_process or args.experiments or args.library_multi_device:
         return "run", None
     world = env.get("WORLD_SIZE")
     if world is not None:
@@ -325,7 +326,7 @@ def bench_handle_request(args, n, rec, db_tensor, device, shard_devices=None,
     validation, the selection expansion, the scan, PirResponse encode and the
     copy of the response to the host.  The database is built from the
     resident rows (device to device).  Returns {Q: ms per request}, and
-    whether both parties' responses reconstruct the record at Q = 1."""
+    whether both parties' responses reconstruct every queried record."""
     from distributed_point_functions_amd import pir as P
     db = P.DenseDpfPirDatabase(shard_devices)
     db.insert_fixed_device(db_tensor, n, rec).build()
@@ -333,17 +334,17 @@ def bench_handle_request(args, n, rec, db_tensor, device, shard_devices=None,
     log_domain = max(0, (n - 1).bit_length())
     dpf = DistributedPointFunction.create(DpfParameters(log_domain, V.XorWrapper(128)))
     rng = np.random.default_rng(77)
-    out, ok = {}, None
+    out, ok = {}, True
     for q in queries:
         idx = [int(i) for i in rng.integers(0, n, q)]
         pairs = P.client_keys(dpf, n, idx, seeds=[(7 + 2 * j, 8 + 2 * j) for j in range(q)])
         req0 = P.pir_request_plain([a for a, _ in pairs])
         r0 = P.parse_response(server.handle_request(req0))  # warm-up
-        if ok is None:
-            r1 = P.parse_response(server.handle_request(
-                P.pir_request_plain([b for _, b in pairs])))
-            want = db_tensor[idx[0] * rec:(idx[0] + 1) * rec].cpu().numpy().tobytes()
-            ok = bytes(x ^ y for x, y in zip(r0[0], r1[0])) == want
+        # both parties' responses reconstruct every queried record
+        r1 = P.parse_response(server.handle_request(P.pir_request_plain([b for _, b in pairs])))
+        for j, i in enumerate(idx):
+            want = db_tensor[i * rec:(i + 1) * rec].cpu().numpy().tobytes()
+            ok = ok and bytes(x ^ y for x, y in zip(r0[j], r1[j])) == want
         reps = max(3, args.steps)
         t0 = time.perf_counter()
         for _ in range(reps):
@@ -386,6 +387,152 @@ def bench_in_process(args):
         hr, ok = bench_handle_request(args, n, rec, src, torch.device("cuda", 0), devs)
         pir = dict(ms=hr, ok=ok, n=n, rec=rec)
     return dict(wall=wall, leaves=total, L=dpf.hierarchy_to_tree(0), pir=pir)
+
+
+GOLDEN_C5 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden",
+                         "c5_subtree_digests.json")
+# torchrun's per-rank variables: the library_multi_device child is one
+# process driving every device, not a rank
+RANK_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+            "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT",
+            "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_RUN_ID",
+            "TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_ERROR_FILE", "TORCH_NCCL_ASYNC_ERROR_HANDLING")
+
+
+def bench_library_multi_device(args):
+    """bench.py --library-multi-device (the child rank 0 starts at world > 1):
+    the library's own multi-device entry points, one process over every
+    device, checked on the spot.
+      * c5: DistributedPointFunction::ExpandLeavesOnDevices of the full 2^32
+        domain over the devices (disjoint subtree slices, one stream per
+        device) for the key tests/golden/c5_subtree_digests.json was made
+        from; sampled 2^20-leaf subtrees of every slice (its first, its last,
+        a random one and alpha's) hashed and compared with the oracle's
+        SHA-256 digests.
+      * c4: a DenseDpfPirDatabase sharded over the devices (rows copied to
+        each shard's device, partials peer-copied to the first device and
+        XOR-folded, csrc/pir.cc) behind DenseDpfPirServer::HandleRequest
+        (pir/dense_dpf_pir_server.cc:92-127) at Q = 1 and 8; both parties'
+        responses reconstruct every queried record.
+    Prints one JSON line {"library_multi_device": {...}}."""
+    import hashlib
+    import random
+    from distributed_point_functions_amd import pir as P
+    devs = [int(d) for d in args.devices.split(",")]
+    with open(GOLDEN_C5) as f:
+        gold = json.load(f)
+    vt = V.Tuple(V.Integer(32), V.IntModN(64, P64))
+    dpf = DistributedPointFunction.create(
+        DpfParameters(gold["log_domain_size"], vt, gold["security_parameter"]))
+    alpha = gold["alpha"]
+    k0, _ = dpf.generate_keys(alpha, tuple(gold["beta"]),
+                              seeds=tuple(int(x) for x in gold["keygen_seeds"]))
+    total = 1 << dpf.hierarchy_to_tree(0)
+    slices = []
+    for i, d in enumerate(devs):
+        lo, hi = sharding.block_range(total, len(devs), i)
+        slices.append((d, lo, hi, torch.empty((hi - lo) * 16, dtype=torch.uint8,
+                                              device=torch.device("cuda", d))))
+    dpf.expand_leaves_on_devices(k0, slices)  # the checked output (and the warm-up)
+    log_sub = gold["log_subtree_leaves"]
+    want = gold["sha256"]["0"]
+    rng = random.Random(2026)
+    checked, bad = 0, []
+    for d, lo, hi, out in slices:
+        first, last = (lo + (1 << log_sub) - 1) >> log_sub, (hi >> log_sub) - 1  # whole subtrees
+        if last < first:
+            continue
+        subs = {first, last, rng.randint(first, last)}
+        if first <= alpha >> log_sub <= last:
+            subs.add(alpha >> log_sub)
+        for sub in sorted(subs):
+            a = ((sub << log_sub) - lo) * 16
+            got = hashlib.sha256(out[a:a + (16 << log_sub)].cpu().numpy()).hexdigest()
+            checked += 1
+            if got != want[sub]:
+                bad.append(sub)
+    for _ in range(max(0, args.warmup - 1)):
+        dpf.expand_leaves_on_devices(k0, slices)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dpf.expand_leaves_on_devices(k0, slices)  # returns when every device is done
+    c5_s = (time.perf_counter() - t0) / args.steps
+    del slices
+    torch.cuda.empty_cache()
+    c5 = {"api": "DistributedPointFunction::ExpandLeavesOnDevices (dpf_amd_expand_leaves_on_devices)",
+          "leaves": total, "ms_per_step": 1e3 * c5_s, "leaves_per_s": total / c5_s,
+          "subtrees_checked": checked, "subtrees_differing": bad,
+          "check": "SHA-256 of sampled 2^%d-leaf subtrees vs tests/golden/c5_subtree_digests.json "
+                   "(oracle)" % log_sub,
+          "correct": checked > 0 and not bad}
+    n, rec = 1 << args.pir_log_records, 256
+    gen = torch.Generator(device=torch.device("cuda", devs[0]))
+    gen.manual_seed(1234)
+    src = torch.randint(0, 256, (n * rec,), dtype=torch.uint8,
+                        device=torch.device("cuda", devs[0]), generator=gen)
+    hr, hr_ok = bench_handle_request(args, n, rec, src, torch.device("cuda", devs[0]), devs,
+                                     queries=(1, 8))
+    del src
+    torch.cuda.empty_cache()
+    c4 = {"api": "DenseDpfPirServer::HandleRequest (dpf_amd_pir_server_handle_request), "
+                 "DenseDpfPirDatabase sharded over the devices",
+          "records": n, "record_bytes": rec,
+          "ms_per_request": {str(q): v for q, v in hr.items()},
+          "db_GBps_at_q1": n * rec / (hr[1] / 1e3) / 1e9,
+          "check": "both parties' responses XOR to every queried record", "correct": hr_ok}
+    return {"devices": devs, "distinct_gpus": len(set(devs)), "force_peer": bool(args.force_peer),
+            "c5": c5, "c4": c4, "correct": bool(c5["correct"] and c4["correct"])}
+
+
+def library_multi_device_cmd(ranks, args):
+    """The child's command line: every rank's device, in rank order; peer
+    copies forced when ranks share a device (a rehearsal of N devices on
+    fewer GPUs), so the cross-device branches still run."""
+    import sys
+    devs = [d for _, d, _ in sorted(ranks)]
+    cmd = [sys.executable, "-u", os.path.abspath(__file__), "--library-multi-device",
+           "--devices", ",".join(str(d) for d in devs), "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--log-domain", str(args.log_domain),
+           "--pir-log-records", str(args.pir_log_records)]
+    if len(set(devs)) < len(devs):
+        cmd.append("--force-peer")
+    return cmd
+
+
+def run_library_multi_device(cmd, timeout_s):
+    """Runs the library_multi_device child (a fresh process: never an exec
+    of this one) and returns its result for the bench line, or — when it
+    fails, hangs past `timeout_s` or prints no result — a dict with
+    correct: false and the error, so the line is always complete."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in RANK_ENV}
+    t0 = time.perf_counter()
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, env=env)
+    except subprocess.TimeoutExpired as e:
+        tail = e.stderr.decode(errors="replace") if isinstance(e.stderr, bytes) else (e.stderr or "")
+        return {"correct": False, "error": "child killed after its %d s limit" % timeout_s,
+                "stderr_tail": tail[-1500:], "child_s": time.perf_counter() - t0}
+    except OSError as e:
+        return {"correct": False, "error": "child could not start: %s" % e}
+    el = time.perf_counter() - t0
+    for line in reversed(p.stdout.splitlines()):
+        if not line.startswith("{"):
+            continue
+        try:
+            d = json.loads(line)
+        except ValueError:
+            continue
+        if isinstance(d, dict) and isinstance(d.get("library_multi_device"), dict):
+            r = d["library_multi_device"]
+            r["child_rc"], r["child_s"] = p.returncode, el
+            if p.returncode != 0:
+                r["correct"] = False
+                r.setdefault("error", "child exit code %d" % p.returncode)
+            return r
+    return {"correct": False, "child_rc": p.returncode, "child_s": el,
+            "error": "child exit code %d without a result line" % p.returncode,
+            "stderr_tail": (p.stderr or "")[-1500:]}
 
 
 def m4_lds_roofline(db_bytes, q, ms, clock_ghz=2.4):
@@ -688,6 +835,13 @@ def main(argv=None):
     ap.add_argument("--in-process", action="store_true",
                     help="drive all --gpus GPUs from this one process through the library's "
                          "multi-GPU API (ExpandLeavesOnDevices, a sharded DenseDpfPirDatabase)")
+    ap.add_argument("--library-multi-device", action="store_true",
+                    help="(the child rank 0 starts at world > 1) time and check the library's own "
+                         "multi-device path over --devices: ExpandLeavesOnDevices (c5) and a "
+                         "sharded DenseDpfPirDatabase behind HandleRequest (c4)")
+    ap.add_argument("--skip-library-multi-device", action="store_true",
+                    help="at world > 1, do not run the library_multi_device child")
+    ap.add_argument("--library-multi-device-timeout", type=int, default=300)
     args = ap.parse_args(argv)
     # torch.cuda.device_count() does not initialise the GPU on this image
     how, what = launch_decision(args, os.environ, torch.cuda.device_count())
@@ -699,6 +853,11 @@ def main(argv=None):
         return spawn_ranks(what, sys.argv[1:] if argv is None else argv)
     if args.experiments:
         return main_experiments(args)
+    if args.library_multi_device:
+        if args.force_peer:
+            _lib.lib().dpf_amd_set_force_peer_copies(1)
+        print(json.dumps({"library_multi_device": bench_library_multi_device(args)}), flush=True)
+        return 0
     if args.in_process:
         if args.force_peer:
             _lib.lib().dpf_amd_set_force_peer_copies(1)
@@ -713,6 +872,7 @@ def main(argv=None):
         cpu = cpu_baseline(args)
     if world > 1:
         dist.barrier()
+    out = None
     if rank == 0:
         leaves = r["leaves"]
         ms = 1000 * r["wall"] / args.steps
@@ -825,9 +985,22 @@ def main(argv=None):
                     "ms_per_request": {str(q): v for q, v in shr.items()},
                     "shard_GBps_at_q1": sn * 256 / (shr[1] / 1e3) / 1e9,
                     "correct": sok}
-        print(json.dumps(out), flush=True)
     if world > 1:
+        # Every rank has freed its buffers (the legs' tensors are gone; the
+        # caching allocator returns them here); then rank 0 starts the
+        # library_multi_device child over all ranks' devices while the other
+        # ranks exit, and folds its result (or its error) into the line.
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        dist.barrier()
         dist.destroy_process_group()
+        if rank == 0:
+            out["library_multi_device"] = (
+                {"skipped": "--skip-library-multi-device"} if args.skip_library_multi_device
+                else run_library_multi_device(library_multi_device_cmd(ranks, args),
+                                              args.library_multi_device_timeout))
+    if rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 def main_in_process(args):

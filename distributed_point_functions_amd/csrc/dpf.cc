@@ -1081,15 +1081,19 @@ StatusOr<EvaluationContext> DistributedPointFunction::CreateEvaluationContext(Dp
 // here; a caller reading the context's field gets host messages built once.
 class ContextDeviceState {
  public:
+  // Freed on a stream the library owns, never the caller's: a context
+  // outlives the stream its EvaluateUntil ran on, and every kernel that wrote
+  // or read the list finished before the state was attached to (or dropped
+  // from) a context — EvaluateUntilOnDevice synchronizes its stream first.
   ~ContextDeviceState() {
     if (buf_ == nullptr) return;
     dpf_internal_host::DeviceGuard g(device_);
-    dpf_internal_host::DevicePool::Get().Free(buf_, stream_);
+    dpf_internal_host::DevicePool::Get().Free(buf_, dpf_internal_host::ThreadStreamOn(device_));
   }
+  // `s`: the stream the list is first written on (allocation only).
   static Status Create(int64_t capacity, hipStream_t s, std::shared_ptr<ContextDeviceState>* out) {
     auto st = std::shared_ptr<ContextDeviceState>(new ContextDeviceState());
     DPF_RETURN_IF_ERROR(HipStatus(hipGetDevice(&st->device_), "hipGetDevice"));
-    st->stream_ = s;
     const int64_t n = std::max<int64_t>(1, capacity);
     const int64_t bytes = 32 * n + ((n + 15) & ~int64_t{15}) + 16;
     DPF_RETURN_IF_ERROR(dpf_internal_host::DevicePool::Get().Alloc(bytes, s, &st->buf_));
@@ -1108,7 +1112,6 @@ class ContextDeviceState {
   int64_t* count_dev() const { return count_dev_; }
   int64_t count() const { return count_; }
   void set_count(int64_t c) { count_ = c; }
-  void set_stream(hipStream_t s) { stream_ = s; }
 
   // The list as host messages, read back on first use (the kernels that
   // wrote it finished before the state was attached to a context).
@@ -1144,7 +1147,6 @@ class ContextDeviceState {
  private:
   ContextDeviceState() = default;
   int device_ = 0;
-  hipStream_t stream_ = nullptr;
   void* buf_ = nullptr;
   char* prefixes_ = nullptr;
   char* seeds_ = nullptr;
@@ -1607,7 +1609,19 @@ Status EvaluateUntilOnDevice(const DpfState& st, int hierarchy_level,
   int* flags = reinterpret_cast<int*>(w + o_flags);
   DPF_RETURN_IF_ERROR(HipStatus(hipMemsetAsync(flags, 0, sizeof(int), s), "hipMemsetAsync"));
   DPF_RETURN_IF_ERROR(ThreadUploadRing().Copy(w + o_p, prefixes.data(), 16 * size_t(n), s));
-  DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(w + o_cw, parts, 9, cw_bytes, coff, s));
+  // the correction words host-written into fine-grained device memory where
+  // the device allows it (one copy kernel and its dispatch gap fewer per
+  // level), else one packed copy; `drain` keeps an early return from reusing
+  // the slot under a running kernel
+  bool cw_placed = false;
+  int cw_slot = -1;
+  char* cwp = nullptr;
+  DPF_RETURN_IF_ERROR(
+      ThreadUploadRing().Place(parts, 9, cw_bytes, coff, &cw_placed, &cw_slot, &cwp));
+  if (!cw_placed) {
+    cwp = w + o_cw;
+    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(cwp, parts, 9, cw_bytes, coff, s));
+  }
   trace.Mark("upload");
   const uint64_t limit[2] = {prev_ld < 64 ? (uint64_t{1} << prev_ld) : 0,
                              prev_ld >= 64 && prev_ld < 128 ? (uint64_t{1} << (prev_ld - 64)) : 0};
@@ -1627,34 +1641,36 @@ Status EvaluateUntilOnDevice(const DpfState& st, int hierarchy_level,
   if (walk_levels > 0)
     DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_seeds(
         n, walk_levels, walk_levels, next->seeds(), next->cbs(), next->prefixes(), 0,
-        w + o_cw + coff[0], reinterpret_cast<const uint8_t*>(w + o_cw + coff[1]),
-        reinterpret_cast<const uint8_t*>(w + o_cw + coff[2]), dpf_amd::kPrgKeyLeftLo,
+        cwp + coff[0], reinterpret_cast<const uint8_t*>(cwp + coff[1]),
+        reinterpret_cast<const uint8_t*>(cwp + coff[2]), dpf_amd::kPrgKeyLeftLo,
         dpf_amd::kPrgKeyLeftHi, dpf_amd::kPrgKeyRightLo, dpf_amd::kPrgKeyRightHi, next->seeds(),
         next->cbs(), s)));
   // each prefix's own node, then its subtree (as the host path's fused branch)
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd::PrefixRoots(
-      n, pidx, plow, bbits, n, next->seeds(), next->cbs(), w + o_cw + coff[3],
-      reinterpret_cast<const uint8_t*>(w + o_cw + coff[4]),
-      reinterpret_cast<const uint8_t*>(w + o_cw + coff[5]), w + o_ps,
+      n, pidx, plow, bbits, n, next->seeds(), next->cbs(), cwp + coff[3],
+      reinterpret_cast<const uint8_t*>(cwp + coff[4]),
+      reinterpret_cast<const uint8_t*>(cwp + coff[5]), w + o_ps,
       reinterpret_cast<uint8_t*>(w + o_pcb), s)));
   void* final_dev = out_on_device ? out : static_cast<void*>(w + o_out);
   DPF_RETURN_IF_ERROR(ClearPadding(vt, final_dev, total * stride, s));
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_expand_and_correct(
-      n, w + o_ps, reinterpret_cast<const uint8_t*>(w + o_pcb), down, w + o_cw + coff[6],
-      reinterpret_cast<const uint8_t*>(w + o_cw + coff[7]),
-      reinterpret_cast<const uint8_t*>(w + o_cw + coff[8]), &vt,
+      n, w + o_ps, reinterpret_cast<const uint8_t*>(w + o_pcb), down, cwp + coff[6],
+      reinterpret_cast<const uint8_t*>(cwp + coff[7]),
+      reinterpret_cast<const uint8_t*>(cwp + coff[8]), &vt,
       reinterpret_cast<const uint64_t*>(corr.data()), ctx.key().party(), cepb, 0, n << down,
       final_dev, s)));
+  if (cw_placed) DPF_RETURN_IF_ERROR(ThreadUploadRing().ReleasePlaced(cw_slot, s));
   DPF_RETURN_IF_ERROR(CopyToHost(readback, flags, sizeof(int), s));
   DPF_RETURN_IF_ERROR(CopyToHost(readback + 1, next->count_dev(), sizeof(int64_t), s));
   trace.Mark("launch");
-  if (!out_on_device)
-    DPF_RETURN_IF_ERROR(CopyToHostSync(out, final_dev, total * stride, s));
-  else
-    DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
+  // The flags first: on a fallback (unsorted, out of range, missing prefix)
+  // the caller's host buffer is left untouched and the host path decides.
+  DPF_RETURN_IF_ERROR(HipStatus(hipStreamSynchronize(s), "sync"));
   drain.Dismiss();
   trace.Mark("sync");
   if (readback[0] != 0) return OkStatus();  // the host path decides
+  if (!out_on_device) DPF_RETURN_IF_ERROR(CopyToHostSync(out, final_dev, total * stride, s));
+  trace.Mark("d2h");
   *fallback = false;
   if (update_ctx) {
     next->set_count(readback[1]);
@@ -1708,8 +1724,7 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
                                     " out of range for hierarchy level " + std::to_string(prev_h));
     return OkStatus();
   };
-  // (the size query, out == nullptr, leaves the check to the evaluation
-  // call that follows it)
+  // (a size query, out == nullptr, runs the serial check before it answers)
   const bool range_deferred =
       out == nullptr || static_cast<int64_t>(prefixes.size()) >= (int64_t{1} << 14);
   if (!range_deferred) DPF_RETURN_IF_ERROR(range_check());
@@ -1727,7 +1742,7 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   const int64_t outputs_per_prefix = int64_t{1} << (log_domain_size - previous_log_domain_size);
   const int64_t total = prefixes.empty() ? outputs_per_prefix : num_prefixes * outputs_per_prefix;
   *num_outputs = total;
-  if (out == nullptr) return OkStatus();
+  if (out == nullptr) return early(OkStatus());
   if (out_capacity < total) return early(InvalidArgumentError("output buffer too small"));
 
   const LevelMeta& m = st.levels[hierarchy_level];
@@ -1864,15 +1879,7 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   uint8_t* root_cb = nullptr;
   PendingContextUpdate pending;
   if (prefixes.empty()) {
-    const uint128 seed = MakeUint128(ctx.key().seed().high(), ctx.key().seed().low());
-    const uint8_t cb = static_cast<uint8_t>(ctx.key().party() != 0);
-    const UploadRing::HostPart parts[2] = {{&seed, 16}, {&cb, 1}};
-    size_t off[2];
-    const size_t bytes = UploadRing::PackedLayout(parts, 2, off);
-    DPF_RETURN_IF_ERROR(roots.Alloc(bytes, s));
-    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(roots.get(), parts, 2, bytes, off, s));
-    root_seeds = roots.as<char>() + off[0];
-    root_cb = reinterpret_cast<uint8_t*>(roots.as<char>() + off[1]);
+    // the key's root goes up with the level's correction words (below)
   } else {
     const bool update_ctx = hierarchy_level < L - 1;
     DPF_RETURN_IF_ERROR(ComputePartialEvaluations(
@@ -1943,10 +1950,33 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
     return OkStatus();
   }
   CwArrays cw = KeyCws(ctx.key(), start_level, stop_level);
-  DeviceBuffer cws, ccl, ccr;
-  DPF_RETURN_IF_ERROR(cws.Upload(cw.seeds.data(), 16 * levels, s));
-  DPF_RETURN_IF_ERROR(ccl.Upload(cw.ccl.data(), levels, s));
-  DPF_RETURN_IF_ERROR(ccr.Upload(cw.ccr.data(), levels, s));
+  // the correction words (and, from the root, the key's seed and control
+  // bit) in one block, host-written into fine-grained device memory where the
+  // device allows it, else one packed copy
+  const uint128 key_seed = MakeUint128(ctx.key().seed().high(), ctx.key().seed().low());
+  const uint8_t key_cb = static_cast<uint8_t>(ctx.key().party() != 0);
+  const UploadRing::HostPart cw_parts[5] = {{cw.seeds.data(), size_t(16) * levels},
+                                            {cw.ccl.data(), size_t(levels)},
+                                            {cw.ccr.data(), size_t(levels)},
+                                            {&key_seed, prefixes.empty() ? size_t{16} : 0},
+                                            {&key_cb, prefixes.empty() ? size_t{1} : 0}};
+  size_t cw_off[5];
+  const size_t cw_bytes = UploadRing::PackedLayout(cw_parts, 5, cw_off);
+  bool cw_placed = false;
+  int cw_slot = -1;
+  char* cwd = nullptr;
+  DPF_RETURN_IF_ERROR(
+      ThreadUploadRing().Place(cw_parts, 5, cw_bytes, cw_off, &cw_placed, &cw_slot, &cwd));
+  DeviceBuffer cw_buf;
+  if (!cw_placed) {
+    DPF_RETURN_IF_ERROR(cw_buf.Alloc(cw_bytes, s));
+    cwd = cw_buf.as<char>();
+    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(cwd, cw_parts, 5, cw_bytes, cw_off, s));
+  }
+  if (prefixes.empty()) {
+    root_seeds = cwd + cw_off[3];
+    root_cb = reinterpret_cast<uint8_t*>(cwd + cw_off[4]);
+  }
   const int64_t num_roots = prefixes.empty() ? 1 : num_unique;
   const int64_t expanded = (num_roots << levels) * cepb;
   const size_t stride = static_cast<size_t>(vt.out_stride);
@@ -1968,9 +1998,12 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   }
   DPF_RETURN_IF_ERROR(ClearPadding(vt, expand_out, expanded * stride, s));
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_expand_and_correct(
-      num_roots, root_seeds, root_cb, levels, cws.get(), ccl.as<uint8_t>(),
-      ccr.as<uint8_t>(), &vt, reinterpret_cast<const uint64_t*>(corr.data()),
-      ctx.key().party(), cepb, 0, num_roots << levels, expand_out, s)));
+      num_roots, root_seeds, root_cb, levels, cwd + cw_off[0],
+      reinterpret_cast<const uint8_t*>(cwd + cw_off[1]),
+      reinterpret_cast<const uint8_t*>(cwd + cw_off[2]), &vt,
+      reinterpret_cast<const uint64_t*>(corr.data()), ctx.key().party(), cepb, 0,
+      num_roots << levels, expand_out, s)));
+  if (cw_placed) DPF_RETURN_IF_ERROR(ThreadUploadRing().ReleasePlaced(cw_slot, s));
 
   trace.Mark("expand_launch");
   void* final_dev = expand_out;
@@ -2309,9 +2342,16 @@ Status DistributedPointFunction::EvaluateAndApplyRaw(Span<const DpfKey* const> k
     size_t off[4];
     const size_t in_bytes = UploadRing::PackedLayout(parts, 4, off);
     DeviceBuffer lvl, dbi;
-    DPF_RETURN_IF_ERROR(lvl.Alloc(in_bytes, s));
-    char* d = lvl.as<char>();
-    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 4, in_bytes, off, s));
+    // host-written into fine-grained device memory where allowed, else one copy
+    bool placed = false;
+    int pslot = -1;
+    char* d = nullptr;
+    DPF_RETURN_IF_ERROR(ThreadUploadRing().Place(parts, 4, in_bytes, off, &placed, &pslot, &d));
+    if (!placed) {
+      DPF_RETURN_IF_ERROR(lvl.Alloc(in_bytes, s));
+      d = lvl.as<char>();
+      DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(d, parts, 4, in_bytes, off, s));
+    }
     if (want_bidx) DPF_RETURN_IF_ERROR(dbi.Upload(bidx.data(), n, s));
     DPF_RETURN_IF_ERROR(ClearPadding(vt, dout.get(), n * vt.out_stride, s));
     const bool first = h == 0;
@@ -2322,6 +2362,7 @@ Status DistributedPointFunction::EvaluateAndApplyRaw(Span<const DpfKey* const> k
         reinterpret_cast<const uint8_t*>(d + off[2]), &vt,
         want_bidx ? dbi.as<uint8_t>() : nullptr, pty.as<int8_t>(), d + off[3], dout.get(),
         h + 1 < H ? state.get() : nullptr, h + 1 < H ? state_cb.as<uint8_t>() : nullptr, s)));
+    if (placed) DPF_RETURN_IF_ERROR(ThreadUploadRing().ReleasePlaced(pslot, s));
     DPF_RETURN_IF_ERROR(
         CopyToHostSync(host_out + h * n * vt.out_stride, dout.get(), n * vt.out_stride, s));
     trace.Mark("level");

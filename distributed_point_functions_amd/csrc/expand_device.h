@@ -735,21 +735,11 @@ int LaunchExpandCoop(hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
 }
 
 // D >= 0: KExpand with DFS depth D; D = -1 / -2 / -3: KExpandCoop with E = 0 / 1 / -2.
-// D = 6 is instantiated only for the PIR selection type (16-byte direct
-// elements), where large batched selection expansions use it.
-template <class Em>
-inline constexpr bool kHasDepth6 = false;
-template <>
-inline constexpr bool kHasDepth6<EmitDirect<16>> = true;
-
 template <class Em>
 int LaunchExpandAnyD(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
   if (D == -1) return LaunchExpandCoop<0, Em>(st, a, vt);
   if (D == -2) return LaunchExpandCoop<1, Em>(st, a, vt);
   if (D == -3) return LaunchExpandCoop<-2, Em>(st, a, vt);
-  if constexpr (kHasDepth6<Em>) {
-    if (D == 6) return LaunchExpand<6, Em>(grid, st, a, vt);
-  }
   switch (D) {
     case 0:
       return LaunchExpand<0, Em>(grid, st, a, vt);
@@ -759,6 +749,8 @@ int LaunchExpandAnyD(int D, int grid, hipStream_t st, const ExpandArgs& a, const
       return LaunchExpand<2, Em>(grid, st, a, vt);
     case 4:
       return LaunchExpand<4, Em>(grid, st, a, vt);
+    case 6:
+      return LaunchExpand<6, Em>(grid, st, a, vt);
     default:
       return LaunchExpand<8, Em>(grid, st, a, vt);
   }

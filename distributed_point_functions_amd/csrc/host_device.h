@@ -375,9 +375,10 @@ class PinnedOut {
 // (device, stream index): the fold that reads them writes them back to zero
 // (dpf_amd::XorFoldClear), so a request needs no memset — one dispatch and
 // its dependent gap, ~10 us of a 0.4 ms shard request — in front of its
-// selection expansion.  A buffer is dirty from Acquire until the caller
-// launches the clearing fold (MarkClean); a dirty one (a request that stopped
-// between its scan and its fold, a new or grown buffer) is zeroed whole by
+// selection expansion.  A buffer is dirty from Acquire until the clearing
+// fold has run and the request's streams synchronized without error
+// (MarkClean); a dirty one (a request that stopped or failed between its
+// scan and the end of its fold, a new or grown buffer) is zeroed whole by
 // the next Acquire.  DPF_AMD_FOLD_CLEAR=0 zeroes on every Acquire (A/B).  The
 // previous user has synchronized.
 class FoldSlots {
@@ -793,8 +794,11 @@ class UploadRing {
   int place_next_ = 0;
 
   // Whether the host can write `device`'s fine-grained memory directly:
-  // large BAR, and a pattern written through the mapping reads back through
-  // the device (checked once per device; DPF_AMD_HOST_WRITE=0 turns it off).
+  // large BAR, and the case Place() relies on — a kernel reading a slot,
+  // the host rewriting it, a kernel reading it again — returns the new bytes
+  // both times (the copy kernel reads the slot into ordinary VRAM, checked
+  // through hipMemcpy; once per device; DPF_AMD_HOST_WRITE=0 turns it off).
+  // Called with `device` current.
   static bool HostWritable(int device) {
     static std::mutex mu;
     static int state[64];  // 0 unknown, 1 yes, 2 no
@@ -805,18 +809,25 @@ class UploadRing {
       const char* e = std::getenv("DPF_AMD_HOST_WRITE");
       int large = 0;
       void* p = nullptr;
+      void* q = nullptr;
       if (!(e && std::strcmp(e, "0") == 0) &&
           hipDeviceGetAttribute(&large, hipDeviceAttributeIsLargeBar, device) == hipSuccess &&
-          large && hipExtMallocWithFlags(&p, 4096, hipDeviceMallocFinegrained) == hipSuccess) {
+          large && hipExtMallocWithFlags(&p, 4096, hipDeviceMallocFinegrained) == hipSuccess &&
+          hipMalloc(&q, 4096) == hipSuccess) {
         uint32_t w[1024], r[1024];
-        for (int i = 0; i < 1024; ++i) w[i] = 0x9e3779b9u * (uint32_t)(i + 1);
-        std::memcpy(p, w, sizeof(w));
-        std::atomic_thread_fence(std::memory_order_seq_cst);
-        if (hipMemcpy(r, p, sizeof(r), hipMemcpyDeviceToHost) == hipSuccess &&
-            std::memcmp(w, r, sizeof(w)) == 0)
-          state[device] = 1;
+        bool ok = true;
+        for (int round = 0; round < 2 && ok; ++round) {
+          for (int i = 0; i < 1024; ++i) w[i] = 0x9e3779b9u * (uint32_t)(i + 1) + (uint32_t)round;
+          std::memcpy(p, w, sizeof(w));
+          std::atomic_thread_fence(std::memory_order_seq_cst);
+          ok = dpf_amd::CopyFromMappedHost(q, p, sizeof(w), nullptr) == DPF_AMD_OK &&
+               hipMemcpy(r, q, sizeof(r), hipMemcpyDeviceToHost) == hipSuccess &&
+               std::memcmp(w, r, sizeof(w)) == 0;
+        }
+        if (ok) state[device] = 1;
       }
       if (p) (void)hipFree(p);
+      if (q) (void)hipFree(q);
       (void)hipGetLastError();  // a refused attribute / allocation is not a launch error
     }
     return state[device] == 1;

@@ -70,14 +70,14 @@ constexpr int64_t kCoopMaxLeaves = int64_t{1} << 22;
 
 // Kernel for a batched expansion of num_keys x range tree leaves
 // (tools/expand_sweep.py batched, profiles/sweep_batched_r03m.log): from 2^23
-// leaves in total KExpand<6> with per-lane keys where the type has it (the
-// PIR selection's 16-byte elements: 64 keys x 2^19 1.09 ms = 0.75 of the LDS
+// leaves in total KExpand<6> with per-lane keys for 16-byte elements (the
+// PIR selection: 64 keys x 2^19 1.09 ms = 0.75 of the LDS
 // bound against KExpand<4> 1.32 and the cooperative 1.42; 16 x 2^19 0.377
 // vs 0.392), else KExpand<4>; KExpandCoop with per-block keys below (8 x
 // 2^19: 0.212 vs D = 4 0.224, D = 6 0.379; 100 x 2^16: 0.316 vs 0.368).
-int BatchedDepth(int64_t num_keys, int64_t range, bool has_depth6) {
+int BatchedDepth(int64_t num_keys, int64_t range, bool wide) {
   const int64_t total = num_keys * range;
-  if (total >= (int64_t{1} << 23) && range >= 64 && has_depth6) return 6;
+  if (total >= (int64_t{1} << 23) && range >= 64 && wide) return 6;
   if (total >= (int64_t{1} << 23) && range >= 16) return 4;
   return CoopDepth(total);
 }
@@ -85,13 +85,6 @@ int BatchedDepth(int64_t num_keys, int64_t range, bool has_depth6) {
 bool SingleDirect(const VtDev& vt) {
   return vt.direct && vt.ns == 1 && vt.sc[0].in_off == 0 && vt.sc[0].out_off == 0 &&
          vt.stride == vt.sc[0].bytes && vt.bn == 1 && vt.epb * vt.sc[0].bytes == 16;
-}
-
-// KExpand<6> exists only for 16-byte direct elements (expand_device.h
-// kHasDepth6); other types take D = 8 for it.
-int ResolveDepth(int D, const VtDev& vt) {
-  if (D == 6 && !(SingleDirect(vt) && vt.sc[0].bytes == 16)) return 8;
-  return D;
 }
 
 KeyPair MakeKeyPair(uint64_t l_lo, uint64_t l_hi, uint64_t r_lo, uint64_t r_hi) {
@@ -321,7 +314,6 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
   const int forced = t_expand_depth;
   if (forced > 0 && forced <= num_levels) D = forced;
   if (forced < 0 && num_levels >= CoopSub(forced)) D = forced;
-  D = ResolveDepth(D, dev);
   if (D > num_levels) D = num_levels >= 4 ? 4 : num_levels;
   ExpandArgs a{};
   a.root_seeds = (const uint4*)root_seeds;
@@ -676,7 +668,6 @@ int ExpandBatched(int64_t num_keys, const void* root_seeds, const uint8_t* root_
   const int forced = t_expand_depth;
   if (forced > 0 && forced <= num_levels) D = forced;
   if (forced < 0) D = forced;
-  D = ResolveDepth(D, dev);
   if (D > num_levels) D = 4;
   const int sub = CoopSub(D);
   ExpandArgs a{};

@@ -321,6 +321,7 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
     hipStream_t s = nullptr;
     bool slots = true;
     dpf_internal_host::FoldSlots::Entry* slot_entry = nullptr;
+    bool fold_cleared = false;  // the clearing fold was enqueued on `s`
     int fold_parts = 0;
     void* buf = nullptr;
     char* sel = nullptr;
@@ -418,7 +419,7 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
       void* fold_out = G == 1 && kout ? kout : g.part;
       if (g.slots) {
         st = AbiStatus(dpf_amd::XorFoldClear(g.ws, g.fold_parts, part_bytes, fold_out, g.s));
-        if (st.ok()) dpf_internal_host::FoldSlots::MarkClean(g.slot_entry);
+        g.fold_cleared = st.ok();  // clean only once the request has synchronized OK
       } else {
         st = AbiStatus(dpf_amd_xor_fold(g.ws, g.fold_parts, part_bytes, fold_out, g.s));
       }
@@ -474,6 +475,11 @@ StatusOr<std::vector<std::string>> DenseDpfPirDatabase::InnerProductSharded(
     if (gather) DevicePool::Get().Free(gather, s0);
     if (folded) DevicePool::Get().Free(folded, s0);
   }
+  // The fold slots count as zeroed only when the fold that cleared them ran
+  // and every stream of the request synchronized without error; otherwise
+  // the next request on them zeroes them first.
+  for (size_t g = 0; g < G; ++g)
+    if (st.ok() && w[g].fold_cleared) dpf_internal_host::FoldSlots::MarkClean(w[g].slot_entry);
   for (size_t g = 0; g < G; ++g) {
     DeviceGuard dg(w[g].device);
     if (w[g].buf) DevicePool::Get().Free(w[g].buf, w[g].s);

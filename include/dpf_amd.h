@@ -380,7 +380,8 @@ int64_t dpf_amd_ctx_num_partial_evaluations(const dpf_amd_ctx* ctx);
 /* EvaluateUntil<T> (h:319-322, 695-891).  `value_type` is the serialized
  * ValueType of T (checked as in h:709-716).  Writes host-layout T values to
  * `out` (capacity in bytes); *num_outputs receives the element count.  With
- * out == NULL only *num_outputs is computed. */
+ * out == NULL only *num_outputs is computed, after the same validation as an
+ * evaluation (arguments, context, and every prefix in range, h:735-745). */
 int dpf_amd_evaluate_until(const dpf_amd_dpf* dpf, int hierarchy_level,
                            const uint64_t* prefixes, int64_t num_prefixes,
                            const uint8_t* value_type, size_t value_type_len,

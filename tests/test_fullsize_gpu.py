@@ -32,6 +32,7 @@ import pytest
 
 from oracle import pyoracle as po
 
+from tests.golden.make_golden import KEY_LEFT, KEY_RIGHT
 from tests.test_kernels_gpu import P64, TYPES, _keys, u8
 
 pytestmark = pytest.mark.gpu
@@ -100,8 +101,9 @@ def _assert_host_layout_equals_words(spec, got: np.ndarray, words: np.ndarray, w
 @pytest.mark.parametrize("depth", [1, 2, 4, 6, 8])
 @pytest.mark.parametrize("spec", TYPES, ids=[repr(t) for t in TYPES])
 def test_forced_depth_matches_oracle(K, cuda, spec, depth):
-    """D = 6 exists for 16-byte direct types (the PIR selection); other
-    types run D = 8 for it."""
+    """Every DFS depth KExpand is instantiated with, every emitter (D = 6
+    included: the batched PIR selection's depth, instantiated for every
+    type since round 6)."""
     d, k0, k1, alpha, beta = _keys(spec, 14, seed=depth)
     assert d.hierarchy_to_tree(0) >= depth
     with K.forced_expand_depth(depth):
@@ -111,17 +113,63 @@ def test_forced_depth_matches_oracle(K, cuda, spec, depth):
             _assert_host_layout_equals_words(spec, got, want, "party %d" % key.party)
 
 
-@pytest.mark.parametrize("depth", [4, 8])
-def test_forced_depth_leaf_ranges(K, cuda, depth):
-    """Ragged leaf ranges that start and end inside a 2^D-leaf subtree."""
-    d, k0, _, _, _ = _keys(C5, 15, seed=3)
-    want = d.evaluate_until_words(0, [], d.create_evaluation_context(k0))
+RANGE_TYPES = [C5, ("int", 64), ("xor", 128)]
+
+
+@pytest.mark.parametrize("depth", [4, 6, 8])
+@pytest.mark.parametrize("spec", RANGE_TYPES, ids=[repr(t) for t in RANGE_TYPES])
+def test_forced_depth_leaf_ranges(K, cuda, spec, depth):
+    """Ragged leaf ranges that start and end inside a 2^D-leaf subtree, both
+    parties (tree leaves; the 8-byte type returns two elements per leaf)."""
+    d, k0, k1, _, _ = _keys(spec, 15, seed=3)
     n = 1 << d.hierarchy_to_tree(0)
     with K.forced_expand_depth(depth):
-        for lo, hi in [(0, n), (1, n - 1), (255, 257), (3000, 3001), (4097, 20000),
-                       (n - 300, n)]:
-            got = _expand(K, cuda, d, k0, C5, lo, hi).cpu().numpy()
-            _assert_host_layout_equals_words(C5, got, want[lo:hi], "[%d, %d)" % (lo, hi))
+        for key in (k0, k1):
+            want = d.evaluate_until_words(0, [], d.create_evaluation_context(key))
+            e = len(want) // n  # elements per tree leaf
+            for lo, hi in [(0, n), (1, n - 1), (63, 65), (255, 257), (3000, 3001),
+                           (4097, 20000), (n - 300, n)]:
+                if hi > n:
+                    continue
+                got = _expand(K, cuda, d, key, spec, lo, hi).cpu().numpy()
+                _assert_host_layout_equals_words(spec, got, want[lo * e:hi * e],
+                                                 "party %d [%d, %d)" % (key.party, lo, hi))
+
+
+@pytest.mark.parametrize("spec", RANGE_TYPES, ids=[repr(t) for t in RANGE_TYPES])
+def test_depth6_many_roots_matches_oracle(K, cuda, spec):
+    """KExpand<6> from many roots with one walk level per thread — the shape
+    of an incremental level (2^k prefix roots, 7 tree levels below each,
+    dpf.cc EvaluateUntilOnDevice) — against the oracle's expansion of the
+    same roots (ExpandSeeds cc:289-372, HashExpandedSeeds cc:523-547)."""
+    import torch
+    from distributed_point_functions_amd import value_types as vtm
+    d, k0, k1, _, _ = _keys(spec, 20, seed=6)
+    L = d.hierarchy_to_tree(0)
+    top = L - 7  # roots at tree level L - 7, 7 levels expanded below each
+    nroots = 1 << top
+    vt = vtm.from_spec(spec)
+    for key in (k0, k1):
+        want = d.evaluate_until_words(0, [], d.create_evaluation_context(key))
+        e = len(want) >> L
+        # the roots themselves: every node of level `top` (oracle walk,
+        # evaluate_prg_hwy.cc:552-634)
+        seeds, cbs = po.evaluate_seeds([key.seed] * nroots, [key.party] * nroots,
+                                       list(range(nroots)), 0, key.cw_seeds()[:top],
+                                       key.ccl()[:top], key.ccr()[:top], KEY_LEFT, KEY_RIGHT,
+                                       top)
+        ka = _key_arrays(K, cuda, d, key)
+        cw = K.u128_tensor(key.cw_seeds()[top:L], cuda)
+        ccl = u8(key.ccl()[top:L], cuda)
+        ccr = u8(key.ccr()[top:L], cuda)
+        for lo, hi in [(0, nroots << 7), (5, (nroots << 7) - 77), (127, 129)]:
+            with K.forced_expand_depth(6):
+                got = K.expand_and_correct(K.u128_tensor(seeds, cuda), u8(cbs, cuda), 7, cw, ccl,
+                                           ccr, vt.descriptor(d.blocks_needed(0)), ka["corr"],
+                                           ka["party"], e, lo, hi)
+            _assert_host_layout_equals_words(spec, got.cpu().numpy(), want[lo * e:hi * e],
+                                             "party %d [%d, %d)" % (key.party, lo, hi))
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("coop", [-1, -2, -3])

@@ -350,7 +350,8 @@ def test_bench_launch_decision():
 
     def a(gpus, **kw):
         return argparse.Namespace(gpus=gpus, in_process=kw.get("ip", False),
-                                  experiments=kw.get("ex", False))
+                                  experiments=kw.get("ex", False),
+                                  library_multi_device=kw.get("lmd", False))
     assert bench.launch_decision(a(1), {}, 1) == ("run", None)
     assert bench.launch_decision(a(8), {}, 8) == ("spawn", 8)
     assert bench.launch_decision(a(8), {"WORLD_SIZE": "8"}, 8) == ("run", None)
@@ -362,6 +363,55 @@ def test_bench_launch_decision():
     assert bench.launch_decision(a(2), {"DPF_AMD_BENCH_BACKEND": "gloo"}, 1) == ("spawn", 2)
     assert bench.launch_decision(a(4, ip=True), {}, 1) == ("run", None)
     assert bench.launch_decision(a(4, ex=True), {}, 1) == ("run", None)
+    assert bench.launch_decision(a(1, lmd=True), {}, 1) == ("run", None)
+
+
+def test_bench_library_multi_device_child_command():
+    """The child covers every rank's device in rank order and forces the
+    peer-copy branches when ranks share a device (the one-GPU rehearsal)."""
+    import argparse
+    import bench
+    args = argparse.Namespace(steps=3, warmup=1, log_domain=32, pir_log_records=26)
+    cmd = bench.library_multi_device_cmd([(1, 1, "b"), (0, 0, "a")], args)
+    assert "--library-multi-device" in cmd and "--force-peer" not in cmd
+    assert cmd[cmd.index("--devices") + 1] == "0,1"
+    cmd = bench.library_multi_device_cmd([(0, 0, "a"), (1, 0, "a")], args)
+    assert cmd[cmd.index("--devices") + 1] == "0,0" and "--force-peer" in cmd
+
+
+def test_bench_library_multi_device_failures_keep_the_line_complete():
+    """Whatever the child does — fails without output, hangs past its limit,
+    prints its result and then fails, or succeeds — the parent returns a dict
+    the bench line can carry, with `correct` and the error when there is one;
+    the rank-specific environment never reaches the child."""
+    import json
+    import sys
+    import bench
+    py = sys.executable
+    r = bench.run_library_multi_device([py, "-c", "import sys; sys.stderr.write('boom'); sys.exit(3)"],
+                                       60)
+    assert r["correct"] is False and r["child_rc"] == 3 and "boom" in r["stderr_tail"]
+    r = bench.run_library_multi_device([py, "-c", "import time; time.sleep(30)"], 1)
+    assert r["correct"] is False and "limit" in r["error"]
+    line = json.dumps({"library_multi_device": {"correct": True, "c5": {}}})
+    r = bench.run_library_multi_device([py, "-c", "print('noise'); print(%r)" % line], 60)
+    assert r["correct"] is True and r["child_rc"] == 0
+    r = bench.run_library_multi_device(
+        [py, "-c", "import sys; print(%r); sys.exit(1)" % line], 60)
+    assert r["correct"] is False and "exit code 1" in r["error"]
+    env_probe = "import os, json; print(json.dumps({'library_multi_device': " \
+                "{'correct': 'RANK' not in os.environ and 'WORLD_SIZE' not in os.environ}}))"
+    old = dict(os.environ)
+    os.environ.update(RANK="0", WORLD_SIZE="2")
+    try:
+        r = bench.run_library_multi_device([py, "-c", env_probe], 60)
+    finally:
+        os.environ.clear()
+        os.environ.update(old)
+    assert r["correct"] is True
+    r = bench.run_library_multi_device(["/nonexistent/python"], 60)
+    assert r["correct"] is False and "could not start" in r["error"]
+    json.dumps(r)
 
 
 def test_bench_spawns_ranks_without_torchrun():

@@ -255,3 +255,116 @@ def test_device_bookkeeping_equals_host_path(api):
                 str(e.value)
         finally:
             L.dpf_amd_set_prefix_expand(prev_mode)
+
+
+def _hip():
+    import ctypes
+    return ctypes.CDLL("libamdhip64.so")
+
+
+def test_context_outlives_the_callers_stream(api):
+    """A context whose partial evaluations were written on a caller-owned
+    stream (dpf_amd_evaluate_until_device's `stream`) is destroyed after that
+    stream: the device-held list is returned on a stream the library owns,
+    and later evaluations on a new caller stream (which may reuse the old
+    handle's address) still match the oracle."""
+    import ctypes
+    import torch
+    from distributed_point_functions_amd import _lib
+    D, V = api
+    hier = [(8, ("int", 64), 0), (16, ("int", 64), 0), (24, ("int", 64), 0)]
+    dpf = _make(api, hier)
+    od = po.Dpf(hier)
+    alpha = 0xA1B2C3
+    k0, _ = dpf.generate_keys_incremental(alpha, [1, 2, 3], seeds=(11, 12))
+    ok0, _ = od.generate_keys(alpha, [1, 2, 3], seeds=(11, 12))
+    L, hip = _lib.lib(), _hip()
+    pre1 = list(range(0, 256, 3))
+    pre2 = sorted({(p << 8) | q for p in pre1[:40] for q in (0, 17, 255)})
+    tp = V.Integer(64).to_proto()
+    for rep in range(3):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        ctx = dpf.create_evaluation_context(k0)
+        octx = od.create_evaluation_context(ok0)
+        for h, pre in ((0, []), (1, pre1)):
+            n = ctypes.c_int64()
+            out = torch.empty(((len(pre) or 1) << 8) * 8, dtype=torch.uint8, device="cuda")
+            pw = po.u128_words(pre) if pre else np.zeros(2, np.uint64)
+            _lib.check(L.dpf_amd_evaluate_until_device(
+                dpf._h, h, pw.ctypes.data_as(ctypes.c_void_p), len(pre), tp, len(tp), ctx._h,
+                ctypes.c_void_p(out.data_ptr()), out.numel(), ctypes.byref(n), s))
+            want = od.evaluate_until_words(h, pre, octx)[:, 0, 0]
+            got = out.cpu().numpy().view(np.uint64)[:n.value]
+            assert np.array_equal(got, want), (rep, h)
+        assert ctx.num_partial_evaluations > 0  # the device-held list of level 1
+        assert hip.hipStreamDestroy(s) == 0
+        del ctx  # after its stream: the list goes back on the library's stream
+        # a fresh context, the thread's own stream: level 2 from level 1's list
+        ctx = dpf.create_evaluation_context(k0)
+        octx = od.create_evaluation_context(ok0)
+        for h, pre in ((0, []), (1, pre1), (2, pre2)):
+            got = _words(dpf.evaluate_until(h, pre, ctx, raw=True), 64)
+            want = od.evaluate_until_words(h, pre, octx)[:, 0, :]
+            assert np.array_equal(got, want), (rep, h)
+    torch.cuda.synchronize()
+
+
+def test_size_query_validates_prefixes(api):
+    """dpf_amd_evaluate_until with out == NULL (the size query) rejects a
+    prefix outside the previous level's domain with the reference's error
+    (h:735-745), for short and for long prefix lists."""
+    import ctypes
+    from distributed_point_functions_amd import _lib
+    D, V = api
+    hier = [(8, ("int", 64), 0), (16, ("int", 64), 0), (24, ("int", 64), 0)]
+    dpf = _make(api, hier)
+    k0, _ = dpf.generate_keys_incremental(77, [1, 2, 3], seeds=(1, 2))
+    L = _lib.lib()
+    tp = V.Integer(64).to_proto()
+    for pre in ([3, 256], list(range(200)) * 100 + [300]):
+        ctx = dpf.create_evaluation_context(k0)
+        dpf.evaluate_until(0, [], ctx)
+        pw = po.u128_words(pre)
+        n = ctypes.c_int64(-1)
+        rc = L.dpf_amd_evaluate_until(dpf._h, 1, pw.ctypes.data_as(ctypes.c_void_p), len(pre),
+                                      tp, len(tp), ctx._h, None, 0, ctypes.byref(n))
+        assert rc == 3
+        msg = L.dpf_amd_last_error().decode()
+        assert "Index %d out of range for hierarchy level 0" % max(pre) in msg, msg
+        # in range: the size query answers
+        ok = [p for p in pre if p < 256][:50]
+        pw = po.u128_words(ok)
+        assert L.dpf_amd_evaluate_until(dpf._h, 1, pw.ctypes.data_as(ctypes.c_void_p), len(ok),
+                                        tp, len(tp), ctx._h, None, 0, ctypes.byref(n)) == 0
+        assert n.value == len(ok) * 256
+
+
+@pytest.mark.parametrize("depth", [4, 6, 8])
+def test_incremental_levels_under_forced_depth(api, depth):
+    """The device incremental path (dpf.cc EvaluateUntilOnDevice: 7 tree
+    levels below each prefix root for uint64 at 8-bit hierarchy steps, c3's
+    shape) with the expansion's DFS depth forced — D = 6 walks one level per
+    thread — every output and the context against the oracle."""
+    from distributed_point_functions_amd import kernels as K
+    hier = [(8, ("int", 64), 0), (16, ("int", 64), 0), (24, ("int", 64), 0), (32, ("int", 64), 0)]
+    dpf = _make(api, hier)
+    od = po.Dpf(hier)
+    alpha = 0x5EEDF00D
+    betas = [3, 5, 7, 9]
+    k0, k1 = dpf.generate_keys_incremental(alpha, betas, seeds=(21, 22))
+    ok0, ok1 = od.generate_keys(alpha, betas, seeds=(21, 22))
+    rng = np.random.default_rng(depth)
+    pre = [[], list(range(256))]
+    for h in (2, 3):
+        parents = sorted(rng.choice(pre[-1], size=min(len(pre[-1]), 1 << 10), replace=False))
+        pre.append(sorted({(int(p) << 8) | int(q) for p in parents for q in rng.integers(0, 256, 4)}))
+    with K.forced_expand_depth(depth):
+        for key, okey in ((k0, ok0), (k1, ok1)):
+            ctx, octx = dpf.create_evaluation_context(key), od.create_evaluation_context(okey)
+            for h in range(4):
+                got = _words(dpf.evaluate_until(h, pre[h], ctx, raw=True), 64)
+                want = od.evaluate_until_words(h, pre[h], octx)[:, 0, :]
+                assert np.array_equal(got, want), (depth, key.party, h)
+                if h < 3:
+                    _same_ctx(ctx, octx)
