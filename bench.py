@@ -559,6 +559,20 @@ def library_sha256():
         return hashlib.sha256(f.read()).hexdigest()
 
 
+def library_identity():
+    """The loaded library: its sha256 (what profiles/ are keyed to), the
+    source hash stamped into it at build time (dpf_amd_version) and whether
+    that is the hash of the csrc/ and include/ in this tree."""
+    from distributed_point_functions_amd import build_native
+    stamped = _lib.lib().dpf_amd_version().decode().rsplit("src:", 1)[-1]
+    try:
+        tree = build_native.source_hash()
+    except OSError:
+        tree = None
+    return {"sha256": library_sha256(), "source_hash": stamped, "tree_source_hash": tree,
+            "matches_sources": stamped == tree}
+
+
 def traffic_from_profiles(kernel_re):
     """(HBM bytes per launch, profile file, PMC entry, error) of the kernel
     whose demangled name matches the regex `kernel_re`, from a committed PMC
@@ -896,6 +910,7 @@ def main(argv=None):
                        "parallelism": "one key's 2^%d domain subtree-sharded over %d GPU(s)" %
                                       (args.log_domain, world)},
             "world_size": world, "backend": bench_backend() if world > 1 else None,
+            "library": library_identity(),
             # (rank, device index, PCI bus id) of every rank
             "rank_devices": ranks,
             # The T-table AES is bound by LDS lookup issue (ds_read_b32: 32
@@ -1042,6 +1057,7 @@ def main_in_process(args):
                      "kernel_ms_is": "step wall time of ExpandLeavesOnDevices",
                      "lookups_per_leaf": LDS_LOOKUPS_PER_LEAF_C5},
         "cpu_baseline": None if args.skip_cpu_baseline else cpu_baseline(args),
+        "library": library_identity(),
     }
     if r["pir"]:
         p = r["pir"]

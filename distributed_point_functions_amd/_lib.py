@@ -160,6 +160,7 @@ def _bind_tier2(L):
     _sig(L, "dpf_amd_pir_db_create", I32, PP)
     _sig(L, "dpf_amd_pir_db_insert", I32, P, P, SZ)
     _sig(L, "dpf_amd_pir_db_insert_fixed", I32, P, P, I64, I64)
+    _sig(L, "dpf_amd_pir_db_insert_packed", I32, P, P, P, I64)
     _sig(L, "dpf_amd_pir_db_build", I32, P)
     _sig(L, "dpf_amd_pir_db_destroy", None, P)
     _sig(L, "dpf_amd_pir_db_size", I64, P)

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import concurrent.futures
 import glob
+import hashlib
 import os
 import re
 import subprocess
@@ -35,6 +36,41 @@ CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
             "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
 
 
+def _hashed_files():
+    """Every file the library is built from: csrc/ and include/ (sorted)."""
+    fs = []
+    for d, pats in ((CSRC, ("*.h", "*.cc", "*.hip")),
+                    (os.path.join(ROOT, "include"), ("*.h", os.path.join("dpf_amd", "*.h")))):
+        for pat in pats:
+            fs += glob.glob(os.path.join(d, pat))
+    return sorted(fs)
+
+
+def source_hash() -> str:
+    """SHA-256 over the library's sources (relative path and bytes of each)
+    and its build flags: what dpf_amd_version() reports after "src:"."""
+    h = hashlib.sha256()
+    h.update(repr((ARCH, CXXFLAGS[:5])).encode())
+    for f in _hashed_files():
+        h.update(os.path.relpath(f, ROOT).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def library_source_hash(path: str = LIB):
+    """The source hash stamped into a built library (read from its bytes,
+    without loading it), or None."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    m = re.search(rb"T-table AES in LDS\) src:([0-9a-f]{64}|unknown)", data)
+    return m.group(1).decode() if m else None
+
+
 def _sources():
     # largest device translation units first so the parallel build ends early
     srcs = glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cc"))
@@ -51,16 +87,15 @@ def _headers_mtime():
 _INCLUDE_RE = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
 
 
-def _deps_mtime(src: str) -> float:
-    """Newest mtime of `src` and the project headers it includes (quoted
-    includes, followed recursively through csrc/ and include/)."""
-    seen, todo, newest = set(), [src], 0.0
+def _deps(src: str):
+    """`src` and the project headers it includes (quoted includes, followed
+    recursively through csrc/ and include/), sorted."""
+    seen, todo = set(), [src]
     while todo:
         f = todo.pop()
         if f in seen:
             continue
         seen.add(f)
-        newest = max(newest, os.path.getmtime(f))
         with open(f, errors="replace") as fh:
             text = fh.read()
         for inc in _INCLUDE_RE.findall(text):
@@ -69,13 +104,24 @@ def _deps_mtime(src: str) -> float:
                 if os.path.exists(cand):
                     todo.append(os.path.normpath(cand))
                     break
-    return newest
+    return sorted(seen)
+
+
+def _object_key(src: str, cmd) -> str:
+    """What an object is built from: its compile command and the bytes of
+    its source and every header it includes."""
+    h = hashlib.sha256("\0".join(cmd).encode())
+    for f in _deps(src):
+        with open(f, "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read() + b"\0")
+    return h.hexdigest()
 
 
 def _compile(src: str, force: bool, obj_dir: str = OBJ_DIR, defines=()) -> str:
+    """Compiles `src` unless its object was built from the same bytes and
+    command (content hashes, not mtimes)."""
     obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
-    if not force and os.path.exists(obj) and os.path.getmtime(obj) >= _deps_mtime(src):
-        return obj
+    stamp = obj + ".key"
     cmd = ["hipcc"] + CXXFLAGS + ["-D" + d for d in defines] + ["-c", src, "-o", obj + ".tmp"]
     if src.endswith(".hip"):
         cmd[1:1] = ["--offload-arch=" + ARCH, "-x", "hip"]
@@ -83,17 +129,30 @@ def _compile(src: str, force: bool, obj_dir: str = OBJ_DIR, defines=()) -> str:
         # host-only C++ (no device pass), HIP runtime API from ROCm
         cmd[1:1] = ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(ROCM, "include"),
                     "-maes", "-msse4.1"]
+    key = _object_key(src, cmd)
+    if not force and os.path.exists(obj) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read() == key:
+                return obj
     subprocess.check_call(cmd)
     os.replace(obj + ".tmp", obj)
+    with open(stamp, "w") as f:
+        f.write(key)
     return obj
 
 
 def build(force: bool = False, jobs: int = 8) -> str:
+    """Compiles the units whose bytes or command changed (content hashes) and
+    relinks whenever the library's stamped source hash is not the tree's — a
+    stale or foreign .so is replaced whatever its mtime."""
     os.makedirs(OBJ_DIR, exist_ok=True)
     srcs = _sources()
+    want = source_hash()
+    # the hash goes into the one unit that defines dpf_amd_version
+    defines = {os.path.join(CSRC, "kernels_capi.cc"): ('DPF_AMD_SOURCE_HASH="%s"' % want,)}
     with concurrent.futures.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), srcs))
-    if (force or not os.path.exists(LIB) or
+        objs = list(ex.map(lambda s: _compile(s, force, defines=defines.get(s, ())), srcs))
+    if (force or not os.path.exists(LIB) or library_source_hash() != want or
             os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs)):
         tmp = LIB + ".tmp%d" % os.getpid()
         subprocess.check_call(["hipcc", "--offload-arch=" + ARCH, "-shared", "-fPIC",

@@ -424,6 +424,25 @@ int dpf_amd_pir_db_insert_fixed(dpf_amd_pir_db* db, const uint8_t* records, int6
   return DPF_AMD_OK;
 }
 
+int dpf_amd_pir_db_insert_packed(dpf_amd_pir_db* db, const uint8_t* data, const int64_t* sizes,
+                                 int64_t num_records) {
+  if (!db->builder) return Fail(DPF_AMD_FAILED_PRECONDITION, "Database already built");
+  if (num_records < 0 || (num_records > 0 && (sizes == nullptr)))
+    return Fail(DPF_AMD_INVALID_ARGUMENT, "bad packed records");
+  int64_t total = 0;
+  for (int64_t i = 0; i < num_records; ++i) {
+    if (sizes[i] < 0) return Fail(DPF_AMD_INVALID_ARGUMENT, "negative record size");
+    total += sizes[i];
+  }
+  if (total > 0 && data == nullptr) return Fail(DPF_AMD_INVALID_ARGUMENT, "bad packed records");
+  const char* p = reinterpret_cast<const char*>(data);
+  for (int64_t i = 0; i < num_records; ++i) {  // Builder::Insert per record, in order
+    db->builder->Insert(std::string(p, static_cast<size_t>(sizes[i])));
+    p += sizes[i];
+  }
+  return DPF_AMD_OK;
+}
+
 int dpf_amd_pir_db_build(dpf_amd_pir_db* db) {
   if (!db->builder) return Fail(DPF_AMD_FAILED_PRECONDITION, "Database already built");
   StatusOr<std::unique_ptr<DenseDpfPirDatabase::Interface>> b = db->builder->Build();

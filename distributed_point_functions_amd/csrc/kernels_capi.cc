@@ -202,7 +202,15 @@ using namespace dpf_amd;
 
 extern "C" {
 
-const char* dpf_amd_version(void) { return "dpf_amd 0.1 (gfx950, T-table AES in LDS)"; }
+// DPF_AMD_SOURCE_HASH: SHA-256 of the sources and build flags this library
+// was compiled from (build_native.source_hash()); build() recompiles when it
+// differs from the tree's, and bench.py reports both.
+#ifndef DPF_AMD_SOURCE_HASH
+#define DPF_AMD_SOURCE_HASH "unknown"
+#endif
+const char* dpf_amd_version(void) {
+  return "dpf_amd 0.1 (gfx950, T-table AES in LDS) src:" DPF_AMD_SOURCE_HASH;
+}
 
 int dpf_amd_device_count(int* count) {
   return HipCheck(hipGetDeviceCount(count), "hipGetDeviceCount");

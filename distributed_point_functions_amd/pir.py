@@ -94,6 +94,19 @@ class DenseDpfPirDatabase:
                                                      a.shape[0], a.shape[1]))
         return self
 
+    def insert_packed(self, data, sizes) -> "DenseDpfPirDatabase":
+        """Bulk insert of records of any sizes: `data` holds them back to
+        back (bytes or a uint8 array), record i is sizes[i] bytes."""
+        a = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) \
+            else np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        sz = np.ascontiguousarray(sizes, dtype=np.int64)
+        if int(sz.sum()) != a.size:
+            raise ValueError("sizes do not add up to the data length")
+        check(_lib.lib().dpf_amd_pir_db_insert_packed(
+            self._h, a.ctypes.data_as(ctypes.c_void_p), sz.ctypes.data_as(ctypes.c_void_p),
+            len(sz)))
+        return self
+
     def insert_fixed_device(self, records, num_records: int, record_size: int) -> "DenseDpfPirDatabase":
         """Bulk insert of records already in device memory (a CUDA uint8
         tensor of num_records * record_size bytes); copied device to device
@@ -134,6 +147,19 @@ class DenseDpfPirDatabase:
 
     def inner_product_with(self, selections: Sequence[Sequence[int]]) -> List[bytes]:
         """InnerProductWith (pir/pir_database_interface.h:65-66)."""
+        if isinstance(selections, np.ndarray):
+            # (q, blocks, 2) uint64 {lo, hi} words: no per-block Python ints
+            if selections.ndim != 3 or selections.shape[2] != 2:
+                raise ValueError("selections array must be (queries, blocks, 2) uint64")
+            q, nb = selections.shape[0], selections.shape[1]
+            if q == 0:
+                return []
+            if nb * BITS_PER_BLOCK < self.size:
+                raise _lib.DpfAmdError(3, "`selections[0]` contains insufficient number of "
+                                          "bits: %d, expected: %d"
+                                       % (nb * BITS_PER_BLOCK, self.size))
+            sel = np.ascontiguousarray(selections, dtype=np.uint64)
+            return self._inner_product_words(sel, nb, q)
         q = len(selections)
         if q == 0:
             return []
@@ -150,6 +176,9 @@ class DenseDpfPirDatabase:
                                           "`selections[0].size()`: actual%d, expected %d"
                                        % (i, len(s_i), nb))
         sel = u128_words([b for s in selections for b in s])
+        return self._inner_product_words(sel, nb, q)
+
+    def _inner_product_words(self, sel: np.ndarray, nb: int, q: int) -> List[bytes]:
         out = np.zeros(max(1, q * self.max_value_size), dtype=np.uint8)
         check(_lib.lib().dpf_amd_pir_db_inner_product(
             self._h, sel.ctypes.data_as(ctypes.c_void_p), nb, q,

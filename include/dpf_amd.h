@@ -78,7 +78,8 @@ typedef struct {
 
 const char* dpf_amd_last_error(void);
 
-/* Library / device info. */
+/* Library / device info.  dpf_amd_version ends in "src:<sha256>", the hash
+ * of the sources and build flags the library was compiled from. */
 int dpf_amd_device_count(int* count);
 const char* dpf_amd_version(void);
 /* Returns the idle device blocks the library's caching allocator holds to
@@ -477,6 +478,10 @@ int dpf_amd_pir_db_insert(dpf_amd_pir_db* db, const uint8_t* record,
 /* Bulk insert of num_records records of equal size. */
 int dpf_amd_pir_db_insert_fixed(dpf_amd_pir_db* db, const uint8_t* records,
                                 int64_t num_records, int64_t record_size);
+/* Bulk insert of num_records records of any sizes, concatenated in `data`
+ * (record i is sizes[i] bytes): Builder::Insert for each, in order. */
+int dpf_amd_pir_db_insert_packed(dpf_amd_pir_db* db, const uint8_t* data,
+                                 const int64_t* sizes, int64_t num_records);
 /* Bulk insert of num_records records of record_size bytes that already live
  * in device memory on `device` (consecutive); Build copies them device to
  * device, never through the host. Must be the only insert of the database. */

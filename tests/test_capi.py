@@ -158,3 +158,14 @@ def test_prefix_expand_and_thread_cache_hooks():
     assert L.dpf_amd_set_thread_cache_cap(-1) == 3
     assert b"cap" in L.dpf_amd_last_error()
     assert L.dpf_amd_set_thread_cache_cap(64) == 0
+
+
+def test_library_is_stamped_with_its_sources():
+    """build() stamps the hash of csrc/ and include/ into the library
+    (dpf_amd_version "... src:<sha256>") and relinks when the loaded one's
+    stamp is not the tree's: the library the tests load is the one these
+    sources build."""
+    from distributed_point_functions_amd import _lib, build_native
+    v = _lib.lib().dpf_amd_version().decode()
+    assert v.rsplit("src:", 1)[-1] == build_native.source_hash()
+    assert build_native.library_source_hash() == build_native.source_hash()

@@ -11,6 +11,9 @@ c3  incremental heavy hitters: 16 levels 8,16,..,128 bits, uint64, 2^16
     surviving prefixes per level (generator of distributed_point_function_
     benchmark.cc:154-191, distinct prefixes); Tier-2 EvaluateNext per level
 c4q dense-PIR XOR scan at Q = 8 and 64 over 2^26 x 256 B (kernel only)
+pirgrid the reference's PIR benchmark grid (dense_dpf_pir_database_benchmark.cc:
+    125-157): 2^16 / 2^20 records x 32 / 256 / 2048 / 16384 B x batch 1 / 2 /
+    10 / 100, scan and InnerProductWith
 dcf DistributedComparisonFunction BatchEvaluate, log_domain 32, uint64
     (distributed_comparison_function_benchmark.cc:31-63 shape): 1024 keys
     via the Tier-2 API, and 2^20 (key, point) pairs through the fused kernel
@@ -303,6 +306,60 @@ def c4q(dev, reps):
     return res
 
 
+GRID_AVGS = (32, 256, 2048, 16384)
+GRID_NS = (1 << 16, 1 << 20)
+GRID_QS = (1, 2, 10, 100)
+
+
+def pirgrid(dev, reps):
+    """The reference's dense-PIR benchmark grid
+    (pir/dense_dpf_pir_database_benchmark.cc:125-157,
+    BM_BatchedInnerProductOnVariableSizeValues): 2^16 / 2^20 records of 32 /
+    256 / 2,048 / 16,384 B on average (sizes in [avg - 8, avg + 8), so rows of
+    AlignBytes(avg + 7) bytes) at batches of 1, 2, 10, 100.  Per case: the
+    scan alone on device-resident selections (HIP events; HBM fraction of
+    rows + selections + results against 8 TB/s), and InnerProductWith through
+    the API (host selections in, host results out; wall clock), whose
+    results must equal the kernel's."""
+    from distributed_point_functions_amd import pir as P
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(125)
+    rows = []
+    for avg in GRID_AVGS:
+        rec = (avg + 7 + 15) // 16 * 16  # AlignBytes of the largest value
+        for n in GRID_NS:
+            db_t = torch.randint(0, 256, (n * rec,), dtype=torch.uint8, device=dev, generator=gen)
+            db = P.DenseDpfPirDatabase()
+            db.insert_fixed_device(db_t, n, rec).build()
+            nb = n // 128
+            for q in GRID_QS:
+                sel = torch.randint(-2**63, 2**63 - 1, (q * nb, 2), dtype=torch.int64, device=dev,
+                                    generator=gen)
+                ws = torch.empty(max(16, _lib.lib().dpf_amd_inner_product_workspace_size(n, rec, q)),
+                                 dtype=torch.uint8, device=dev)
+                out = torch.empty(q * rec, dtype=torch.uint8, device=dev)
+
+                def scan():
+                    kernels.inner_product(db_t, n, rec, sel, q, ws, out)
+                t = ev_time(scan, reps)
+                host_sel = sel.cpu().numpy().view(np.uint64).reshape(q, nb, 2)
+                api_res = []
+                ta = wall_time(lambda: api_res.append(db.inner_product_with(host_sel)), reps)
+                same = b"".join(api_res[-1]) == out.cpu().numpy().reshape(q, rec)[:, :rec].tobytes()
+                algo = n * rec + q * nb * 16 + q * rec
+                rows.append({"records": n, "avg_bytes": avg, "row_bytes": rec, "batch": q,
+                             "scan_ms": t * 1e3, "scan_db_GBps": n * rec / t / 1e9,
+                             "hbm_frac": algo / t / 8e12, "api_ms": ta * 1e3,
+                             "api_db_GBps": n * rec / ta / 1e9, "api_equals_scan": same})
+                del ws, sel, out
+            del db, db_t
+            torch.cuda.empty_cache()
+    return {"config": "pirgrid",
+            "workload": "dense_dpf_pir_database_benchmark.cc:125-157 grid (records x avg bytes x "
+                        "batch), scan and InnerProductWith",
+            "rows": rows}
+
+
 def stride(dev, reps):
     """Dense scan at 2^26 rows with the reference's 16-byte-aligned row
     stride vs the same rows padded to a power-of-two / 1 KiB-multiple width,
@@ -498,8 +555,15 @@ def main():
     ap.add_argument("--c4q-queries", default=None, help="comma list, e.g. 64 (profiling)")
     ap.add_argument("--no-ab", action="store_true", help="c4q: skip the kernel A/B")
     ap.add_argument("--c2-batched-only", action="store_true", help="c2: the batched kernel only")
+    ap.add_argument("--grid", default=None,
+                    help="pirgrid subset as avg:n:q lists, e.g. 16384:1048576:1 (profiling)")
     args = ap.parse_args()
-    global C4Q_QUERIES, C4Q_AB, C2_BATCHED_ONLY
+    global C4Q_QUERIES, C4Q_AB, C2_BATCHED_ONLY, GRID_AVGS, GRID_NS, GRID_QS
+    if args.grid:
+        a, n, q = args.grid.split(":")
+        GRID_AVGS = tuple(int(x) for x in a.split(","))
+        GRID_NS = tuple(int(x) for x in n.split(","))
+        GRID_QS = tuple(int(x) for x in q.split(","))
     C2_BATCHED_ONLY = args.c2_batched_only
     if args.c4q_queries:
         C4Q_QUERIES = tuple(int(x) for x in args.c4q_queries.split(","))

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Profiling recipe run on the GPU box.
 # Usage: bash tools/profile_gpu.sh <tag> [bench args...]
+#        PROF_SCRIPT=tools/bench_configs.py bash tools/profile_gpu.sh <tag> <its args...>
 # Trace pass first, then one PMC pass per counter group (never combined with
 # tracing).  Stops at the first abnormal exit (fault / abort / timeout).
 TAG=${1:-r01}; shift
@@ -12,7 +13,7 @@ mkdir -p $OUT
 sha256sum ${DPF_AMD_LIB:-distributed_point_functions_amd/_native/libdpf_amd.so} | cut -d" " -f1 > $OUT/library.sha256
 run() {  # name, timeout, rocprof args...
   local name=$1 to=$2; shift 2
-  timeout -k 10 $to rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 bench.py $ARGS > $OUT/$name.log 2>&1
+  timeout -k 10 $to rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 ${PROF_SCRIPT:-bench.py} $ARGS > $OUT/$name.log 2>&1
   local rc=$?
   echo "$name rc=$rc"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
