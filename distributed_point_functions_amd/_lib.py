@@ -112,6 +112,7 @@ def lib():
     _sig(L, "dpf_amd_set_expand_depth", I32, I32)
     _sig(L, "dpf_amd_set_expand_roots", I32, I32)
     _sig(L, "dpf_amd_set_scan_m4", I32, I32)
+    _sig(L, "dpf_amd_set_scan_skip_unselected", I32, I32)
     _sig(L, "dpf_amd_set_walk_mode", I32, I32)
     _sig(L, "dpf_amd_set_dcf_kernel", I32, I32)
     _sig(L, "dpf_amd_set_prefix_expand", I32, I32)

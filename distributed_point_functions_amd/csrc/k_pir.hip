@@ -286,19 +286,26 @@ __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
     } else {
 #pragma unroll 1
       for (int d = 0; d < 4; ++d) {
-        // selection word d (records rec0 + 32d ..) of each query
+        // selection word d (records rec0 + 32d ..) of each query; with the
+        // opt-in skip (ScanArgs::skip) their union masks the loads, so a
+        // record no query of the pass selects is never fetched
         uint32_t word[QN];
+        uint32_t need = a.skip ? 0u : ~0u;
 #pragma unroll
-        for (int q = 0; q < QN; ++q)
+        for (int q = 0; q < QN; ++q) {
           word[q] = (q < a.nq) ? sel[((int64_t)(a.q0 + q) * a.sel_blocks + tile) * 4 + d] : 0u;
+          need |= word[q];
+        }
 #pragma unroll 1
         for (int k0 = 0; k0 < 32; k0 += G * U) {
           uint4 v[U];
 #pragma unroll
           for (int u = 0; u < U; ++u) {
-            const int64_t rec = rec0 + d * 32 + k0 + u * G + my_rec;
-            v[u] = (full || rec < a.num_records) ? LoadRecordWord(&a.db[rec * a.C + my_chunk])
-                                                  : make_uint4(0, 0, 0, 0);
+            const int bit = k0 + u * G + my_rec;
+            const int64_t rec = rec0 + d * 32 + bit;
+            v[u] = ((full || rec < a.num_records) && ((need >> bit) & 1u))
+                       ? LoadRecordWord(&a.db[rec * a.C + my_chunk])
+                       : make_uint4(0, 0, 0, 0);
           }
 #pragma unroll
           for (int u = 0; u < U; ++u) {

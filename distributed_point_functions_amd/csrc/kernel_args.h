@@ -150,6 +150,12 @@ struct ScanArgs {
   // atomically into partial slot b % S (zeroed before the scan), so the fold
   // reads S partials instead of one per block.
   int32_t slots;
+  // KPirScanG (records of 32 B and more): 0 (default) = every record is
+  // read, an access pattern independent of the selection; 1 (opt-in,
+  // DPF_AMD_SCAN_SKIP_UNSELECTED=1) = a record no query of the pass selects
+  // is not read, as the reference's scan skips it (inner_product_hwy.cc:
+  // 213-221) — the access pattern then follows the selection share.
+  int32_t skip;
 };
 
 // Fold slots of the masked scan when a pass's partial is small: 64 slots,

@@ -39,6 +39,15 @@ const int kScanM4Default = [] {
   return e ? std::atoi(e) : -1;
 }();
 thread_local int t_scan_m4 = kScanM4Default;
+// dpf_amd_set_scan_skip_unselected (opt-in): the masked scan reads only the
+// records some query of the pass selects, as the reference's scan does
+// (inner_product_hwy.cc:213-221).  Off by default: every record is read, so
+// the scan's access pattern does not depend on the selection share.
+const int kScanSkipDefault = [] {
+  const char* e = std::getenv("DPF_AMD_SCAN_SKIP_UNSELECTED");
+  return (e && std::atoi(e) != 0) ? 1 : 0;
+}();
+thread_local int t_scan_skip = kScanSkipDefault;
 
 int GridFor(int64_t items, int block, int max_blocks) {
   int64_t g = (items + block - 1) / block;
@@ -464,6 +473,13 @@ int dpf_amd_set_walk_mode(int mode) {
   return old;
 }
 
+int dpf_amd_set_scan_skip_unselected(int on) {
+  if (on != 0 && on != 1) return -2;
+  const int old = t_scan_skip;
+  t_scan_skip = on;
+  return old;
+}
+
 int dpf_amd_set_scan_m4(int mode) {
   if (mode < -1 || mode > 1) return -2;
   const int old = t_scan_m4;
@@ -643,6 +659,7 @@ int ScanPiece(const void* db, int64_t num_records, int64_t record_stride,
   a.parts = grid;
   a.qgroups = 1;
   a.slots = plan.slots ? kScanSlots : 0;
+  a.skip = t_scan_skip;
   const dim3 g(grid, (C + 63) / 64);
   for (int q0 = 0; q0 < num_queries;) {
     const int rem = num_queries - q0;

@@ -179,6 +179,25 @@ class forced_scan_m4:
         _lib.lib().dpf_amd_set_scan_m4(self.prev)
 
 
+class scan_skip_unselected:
+    """Context manager for the opt-in scan that reads only selected records
+    (dpf_amd_set_scan_skip_unselected: 1 skip, as the reference's scan; 0
+    read every record, the default)."""
+
+    def __init__(self, on: int = 1):
+        self.on = int(on)
+
+    def __enter__(self):
+        prev = _lib.lib().dpf_amd_set_scan_skip_unselected(self.on)
+        if prev < 0:
+            raise ValueError("scan skip must be 0 or 1")
+        self.prev = prev
+        return self
+
+    def __exit__(self, *exc):
+        _lib.lib().dpf_amd_set_scan_skip_unselected(self.prev)
+
+
 class forced_walk_mode:
     """Context manager selecting the point-walk kernel of this thread
     (dpf_amd_set_walk_mode: 0 automatic, 1 four lanes per point, 2 one lane

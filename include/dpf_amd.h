@@ -198,6 +198,17 @@ int dpf_amd_set_expand_roots(int mode);
  * Returns the previous setting, or -2 for an invalid mode (unchanged). */
 int dpf_amd_set_scan_m4(int mode);
 
+/* Opt-in (calling thread only): 1 = the masked XOR scan (dpf_amd_inner_product,
+ * InnerProductWith, HandleRequest; records of >= 32 bytes) reads only the
+ * records some query of a pass selects, as the reference's InnerProduct
+ * skips unselected records (inner_product_hwy.cc:213-221) — about half the
+ * table at one query; the scan's memory access pattern then follows the
+ * selection share.  0 (the default) = every record is read, an access
+ * pattern independent of the selection.  Every thread starts from
+ * DPF_AMD_SCAN_SKIP_UNSELECTED (or 0).  Returns the previous setting, or -2
+ * for an invalid value (unchanged). */
+int dpf_amd_set_scan_skip_unselected(int on);
+
 /* Test hook: the calling thread's point-walk kernel (EvaluateAt /
  * EvaluateAndApply / the batched point evaluation).  0 = automatic (four
  * lanes per point below 65,536 points for types of <= 256 bits, one lane per

@@ -406,7 +406,7 @@ SCAN_CASES = [(1, 16, 1), (1000, 256, 1), (1000, 256, 3), (4096, 80, 8), (300, 1
               (40000, 16, 5)]
 
 
-def _scan_case(K, cuda, n, size, q, mode):
+def _scan_case(K, cuda, n, size, q, mode, skip=0):
     import torch
     rng = np.random.default_rng(n * 7 + size)
     stride = (size + 15) // 16 * 16
@@ -419,7 +419,7 @@ def _scan_case(K, cuda, n, size, q, mode):
     sels = [[(int(sel_words[k * blocks + i, 0]) & M64) | ((int(sel_words[k * blocks + i, 1]) & M64) << 64)
              for i in range(blocks)] for k in range(q)]
     want = po.inner_product([bytes(r) for r in recs], sels)
-    with K.forced_scan_m4(mode):
+    with K.forced_scan_m4(mode), K.scan_skip_unselected(skip):
         out = K.inner_product(torch.from_numpy(db).to(cuda), n, stride,
                               torch.from_numpy(sel_words).to(cuda), q)
     got = out.cpu().numpy().reshape(q, stride)[:, :size]
@@ -439,6 +439,72 @@ def test_inner_product_each_scan_kernel(K, cuda, n, size, q, mode):
     """Masked scan (KPirScanG) and Four-Russians scan (KPirScanM4) forced on
     every shape, including the ones the automatic choice never gives them."""
     _scan_case(K, cuda, n, size, q, mode)
+
+
+@pytest.mark.parametrize("n,size,q", SCAN_CASES)
+def test_inner_product_skipping_unselected_records(K, cuda, n, size, q):
+    """The opt-in scan that reads only the records a pass selects (the
+    reference's skip, inner_product_hwy.cc:213-221) answers as the oracle on
+    every shape, masked scan forced (the Four-Russians passes are unchanged)."""
+    _scan_case(K, cuda, n, size, q, 0, skip=1)
+
+
+def test_inner_product_skip_sparse_and_empty_selections(K, cuda):
+    """Skipping with selections of a few bits and of none: only the selected
+    rows reach the sums, an all-zero selection gives zeros."""
+    import torch
+    n, size = 5003, 272
+    rng = np.random.default_rng(3)
+    db = rng.integers(0, 256, size=(n, size), dtype=np.uint8)
+    blocks = (n + 127) // 128
+    picks = [[], [0], [n - 1], [5, 77, 4095, 4096, 5002]]
+    sels = []
+    for p in picks:
+        v = [0] * blocks
+        for r in p:
+            v[r // 128] |= 1 << (r % 128)
+        sels.append(v)
+    words = np.array([[v & M64, v >> 64] for s in sels for v in s], dtype=np.uint64).view(np.int64)
+    with K.forced_scan_m4(0), K.scan_skip_unselected(1):
+        out = K.inner_product(torch.from_numpy(db.reshape(-1)).to(cuda), n, size,
+                              torch.from_numpy(words).to(cuda), len(sels))
+    got = out.cpu().numpy().reshape(len(sels), size)
+    for k, p in enumerate(picks):
+        want = np.zeros(size, np.uint8)
+        for r in p:
+            want ^= db[r]
+        assert np.array_equal(got[k], want), p
+
+
+def test_handle_request_with_scan_skip_reconstructs(K, cuda):
+    """HandleRequest on this thread with the skip on: both parties' answers
+    still XOR to the records (a plain server, 3 queries)."""
+    from distributed_point_functions_amd import pir as P
+    from distributed_point_functions_amd import value_types as V
+    from distributed_point_functions_amd.dpf import DistributedPointFunction, DpfParameters
+    n, size = 20000, 256
+    rng = np.random.default_rng(11)
+    recs = rng.integers(0, 256, size=(n, size), dtype=np.uint8)
+    servers = []
+    for _ in range(2):
+        db = P.DenseDpfPirDatabase()
+        db.insert_fixed(recs)
+        servers.append(P.DenseDpfPirServer.create_plain(n, db))
+    dpf = DistributedPointFunction.create(DpfParameters((n - 1).bit_length(), V.XorWrapper(128)))
+    idx = [0, 12345, n - 1]
+    pairs = P.client_keys(dpf, n, idx, seeds=[(1 + j, 50 + j) for j in range(3)])
+    with K.scan_skip_unselected(1):
+        r0 = P.parse_response(servers[0].handle_request(P.pir_request_plain([a for a, _ in pairs])))
+        r1 = P.parse_response(servers[1].handle_request(P.pir_request_plain([b for _, b in pairs])))
+    for j, i in enumerate(idx):
+        assert bytes(x ^ y for x, y in zip(r0[j], r1[j])) == recs[i].tobytes()
+
+
+def test_scan_skip_knob_validates():
+    from distributed_point_functions_amd import kernels as K
+    with pytest.raises(ValueError):
+        with K.scan_skip_unselected(2):
+            pass
 
 
 @pytest.mark.parametrize("n,size,qs", [(1 << 22, 256, (16, 40, 64, 100)),
