@@ -286,6 +286,32 @@ def bench_pir(args, world, rank, device):
     barrier(world)
     wall = max_over_ranks(time.perf_counter() - t0, world) / args.steps
     scan_ms = max_over_ranks(scan_ms / args.steps, world)
+    # The opt-in scan that reads only the selected records, as the
+    # reference's InnerProduct does (inner_product_hwy.cc:213-221; the access
+    # pattern then follows the selection share): reported beside the
+    # default constant-time scan, never as the line's figures.
+    skip = None
+    if not args.skip_scan_skip:
+        with kernels.scan_skip_unselected(1):
+            a2 = query(keys[0]).clone()
+            b2 = query(keys[1]).clone()
+            sok = bool(torch.equal(a2 ^ b2, rec_idx))
+            query(keys[0])
+            nsel = int(np.unpackbits(sel.cpu().numpy()).sum())  # this rank's selected rows
+            for _ in range(args.warmup):
+                query(keys[0])
+            barrier(world)
+            sms = 0.0
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                query(keys[0], timed_scan=True)
+                torch.cuda.synchronize()
+                sms += scan_ev[0].elapsed_time(scan_ev[1])
+            barrier(world)
+            swall = max_over_ranks(time.perf_counter() - t0, world) / args.steps
+            sms = max_over_ranks(sms / args.steps, world)
+        skip = dict(ok=sok, wall_s=swall, scan_ms=sms, selected_rows=nsel,
+                    read_bytes=nsel * rec + (b_hi - b_lo) * 16)
     # a 64-query batch over the same resident rows (the reference batches up
     # to 100 queries: pir/dense_dpf_pir_database_benchmark.cc): the
     # Four-Russians scan (KPirScanM4), random selection shares
@@ -316,7 +342,7 @@ def bench_pir(args, world, rank, device):
             shard = (n // 8, bench_handle_request(args, n // 8, rec, db[:(n // 8) * rec], device,
                                                   queries=(1, 8)))
     return dict(ok=ok, wall_s=wall, scan_ms=scan_ms, db_bytes=n * rec, per_gpu_bytes=per * rec,
-                records=n, mq=mq, mq_ms=mq_ms, hr=hr, shard=shard)
+                records=n, mq=mq, mq_ms=mq_ms, hr=hr, shard=shard, skip=skip)
 
 
 def bench_handle_request(args, n, rec, db_tensor, device, shard_devices=None,
@@ -350,6 +376,15 @@ def bench_handle_request(args, n, rec, db_tensor, device, shard_devices=None,
         for _ in range(reps):
             server.handle_request(req0)
         out[q] = 1e3 * (time.perf_counter() - t0) / reps
+        if q == 1 and not getattr(args, "skip_scan_skip", True):
+            # the same request with the opt-in skip of unselected records
+            with kernels.scan_skip_unselected(1):
+                s0 = P.parse_response(server.handle_request(req0))
+                ok = ok and s0 == r0
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    server.handle_request(req0)
+                out["1_skip_unselected"] = 1e3 * (time.perf_counter() - t0) / reps
     del server, db
     return out, ok
 
@@ -837,6 +872,8 @@ def main(argv=None):
     ap.add_argument("--skip-cpu-baseline", action="store_true")
     ap.add_argument("--skip-pir", action="store_true")
     ap.add_argument("--skip-handle-request", action="store_true")
+    ap.add_argument("--skip-scan-skip", action="store_true",
+                    help="do not time the opt-in scan that reads only selected records")
     ap.add_argument("--devices", default="",
                     help="--in-process: comma-separated device list, one slice / shard per entry "
                          "(entries may repeat: a rehearsal of N devices' code on fewer GPUs)")
@@ -984,6 +1021,24 @@ def main(argv=None):
                                                     pir["mq_ms"]),
                     "kernel": "KPirScanM4<1>+KXorFold (scan only, no selection DPF)"},
             }
+            if pir.get("skip"):
+                sk = pir["skip"]
+                read_gbs = sk["read_bytes"] / (sk["scan_ms"] / 1e3) / 1e9
+                out["pir"]["skip_unselected"] = {
+                    "opt_in": "dpf_amd_set_scan_skip_unselected(1): the scan reads only the "
+                              "selected records, as the reference's InnerProduct skips the others "
+                              "(inner_product_hwy.cc:213-221); its access pattern follows the "
+                              "selection share, so the default scan above reads every record",
+                    "ms_per_query": 1e3 * sk["wall_s"], "scan_ms": sk["scan_ms"],
+                    "db_GBps": pir["db_bytes"] / sk["wall_s"] / 1e9,
+                    "scan_db_GBps": pir["per_gpu_bytes"] / (sk["scan_ms"] / 1e3) / 1e9,
+                    "selected_rows_rank0": sk["selected_rows"],
+                    "roofline": {"bound": "hbm", "achieved": read_gbs, "peak": HBM_PEAK_GBS,
+                                 "unit": "GB/s", "frac": read_gbs / HBM_PEAK_GBS,
+                                 "algorithmic_bytes": sk["read_bytes"],
+                                 "algorithmic_is": "selected rows x 256 B + selection blocks "
+                                                   "(rank 0)"},
+                    "correct": sk["ok"]}
             if pir.get("hr"):
                 hr, hr_ok = pir["hr"]
                 out["pir"]["handle_request"] = {

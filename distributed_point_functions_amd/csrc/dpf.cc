@@ -1609,19 +1609,7 @@ Status EvaluateUntilOnDevice(const DpfState& st, int hierarchy_level,
   int* flags = reinterpret_cast<int*>(w + o_flags);
   DPF_RETURN_IF_ERROR(HipStatus(hipMemsetAsync(flags, 0, sizeof(int), s), "hipMemsetAsync"));
   DPF_RETURN_IF_ERROR(ThreadUploadRing().Copy(w + o_p, prefixes.data(), 16 * size_t(n), s));
-  // the correction words host-written into fine-grained device memory where
-  // the device allows it (one copy kernel and its dispatch gap fewer per
-  // level), else one packed copy; `drain` keeps an early return from reusing
-  // the slot under a running kernel
-  bool cw_placed = false;
-  int cw_slot = -1;
-  char* cwp = nullptr;
-  DPF_RETURN_IF_ERROR(
-      ThreadUploadRing().Place(parts, 9, cw_bytes, coff, &cw_placed, &cw_slot, &cwp));
-  if (!cw_placed) {
-    cwp = w + o_cw;
-    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(cwp, parts, 9, cw_bytes, coff, s));
-  }
+  DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(w + o_cw, parts, 9, cw_bytes, coff, s));
   trace.Mark("upload");
   const uint64_t limit[2] = {prev_ld < 64 ? (uint64_t{1} << prev_ld) : 0,
                              prev_ld >= 64 && prev_ld < 128 ? (uint64_t{1} << (prev_ld - 64)) : 0};
@@ -1641,25 +1629,24 @@ Status EvaluateUntilOnDevice(const DpfState& st, int hierarchy_level,
   if (walk_levels > 0)
     DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_evaluate_seeds(
         n, walk_levels, walk_levels, next->seeds(), next->cbs(), next->prefixes(), 0,
-        cwp + coff[0], reinterpret_cast<const uint8_t*>(cwp + coff[1]),
-        reinterpret_cast<const uint8_t*>(cwp + coff[2]), dpf_amd::kPrgKeyLeftLo,
+        w + o_cw + coff[0], reinterpret_cast<const uint8_t*>(w + o_cw + coff[1]),
+        reinterpret_cast<const uint8_t*>(w + o_cw + coff[2]), dpf_amd::kPrgKeyLeftLo,
         dpf_amd::kPrgKeyLeftHi, dpf_amd::kPrgKeyRightLo, dpf_amd::kPrgKeyRightHi, next->seeds(),
         next->cbs(), s)));
   // each prefix's own node, then its subtree (as the host path's fused branch)
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd::PrefixRoots(
-      n, pidx, plow, bbits, n, next->seeds(), next->cbs(), cwp + coff[3],
-      reinterpret_cast<const uint8_t*>(cwp + coff[4]),
-      reinterpret_cast<const uint8_t*>(cwp + coff[5]), w + o_ps,
+      n, pidx, plow, bbits, n, next->seeds(), next->cbs(), w + o_cw + coff[3],
+      reinterpret_cast<const uint8_t*>(w + o_cw + coff[4]),
+      reinterpret_cast<const uint8_t*>(w + o_cw + coff[5]), w + o_ps,
       reinterpret_cast<uint8_t*>(w + o_pcb), s)));
   void* final_dev = out_on_device ? out : static_cast<void*>(w + o_out);
   DPF_RETURN_IF_ERROR(ClearPadding(vt, final_dev, total * stride, s));
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_expand_and_correct(
-      n, w + o_ps, reinterpret_cast<const uint8_t*>(w + o_pcb), down, cwp + coff[6],
-      reinterpret_cast<const uint8_t*>(cwp + coff[7]),
-      reinterpret_cast<const uint8_t*>(cwp + coff[8]), &vt,
+      n, w + o_ps, reinterpret_cast<const uint8_t*>(w + o_pcb), down, w + o_cw + coff[6],
+      reinterpret_cast<const uint8_t*>(w + o_cw + coff[7]),
+      reinterpret_cast<const uint8_t*>(w + o_cw + coff[8]), &vt,
       reinterpret_cast<const uint64_t*>(corr.data()), ctx.key().party(), cepb, 0, n << down,
       final_dev, s)));
-  if (cw_placed) DPF_RETURN_IF_ERROR(ThreadUploadRing().ReleasePlaced(cw_slot, s));
   DPF_RETURN_IF_ERROR(CopyToHost(readback, flags, sizeof(int), s));
   DPF_RETURN_IF_ERROR(CopyToHost(readback + 1, next->count_dev(), sizeof(int64_t), s));
   trace.Mark("launch");
@@ -1879,7 +1866,15 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   uint8_t* root_cb = nullptr;
   PendingContextUpdate pending;
   if (prefixes.empty()) {
-    // the key's root goes up with the level's correction words (below)
+    const uint128 seed = MakeUint128(ctx.key().seed().high(), ctx.key().seed().low());
+    const uint8_t cb = static_cast<uint8_t>(ctx.key().party() != 0);
+    const UploadRing::HostPart parts[2] = {{&seed, 16}, {&cb, 1}};
+    size_t off[2];
+    const size_t bytes = UploadRing::PackedLayout(parts, 2, off);
+    DPF_RETURN_IF_ERROR(roots.Alloc(bytes, s));
+    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(roots.get(), parts, 2, bytes, off, s));
+    root_seeds = roots.as<char>() + off[0];
+    root_cb = reinterpret_cast<uint8_t*>(roots.as<char>() + off[1]);
   } else {
     const bool update_ctx = hierarchy_level < L - 1;
     DPF_RETURN_IF_ERROR(ComputePartialEvaluations(
@@ -1950,33 +1945,10 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
     return OkStatus();
   }
   CwArrays cw = KeyCws(ctx.key(), start_level, stop_level);
-  // the correction words (and, from the root, the key's seed and control
-  // bit) in one block, host-written into fine-grained device memory where the
-  // device allows it, else one packed copy
-  const uint128 key_seed = MakeUint128(ctx.key().seed().high(), ctx.key().seed().low());
-  const uint8_t key_cb = static_cast<uint8_t>(ctx.key().party() != 0);
-  const UploadRing::HostPart cw_parts[5] = {{cw.seeds.data(), size_t(16) * levels},
-                                            {cw.ccl.data(), size_t(levels)},
-                                            {cw.ccr.data(), size_t(levels)},
-                                            {&key_seed, prefixes.empty() ? size_t{16} : 0},
-                                            {&key_cb, prefixes.empty() ? size_t{1} : 0}};
-  size_t cw_off[5];
-  const size_t cw_bytes = UploadRing::PackedLayout(cw_parts, 5, cw_off);
-  bool cw_placed = false;
-  int cw_slot = -1;
-  char* cwd = nullptr;
-  DPF_RETURN_IF_ERROR(
-      ThreadUploadRing().Place(cw_parts, 5, cw_bytes, cw_off, &cw_placed, &cw_slot, &cwd));
-  DeviceBuffer cw_buf;
-  if (!cw_placed) {
-    DPF_RETURN_IF_ERROR(cw_buf.Alloc(cw_bytes, s));
-    cwd = cw_buf.as<char>();
-    DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(cwd, cw_parts, 5, cw_bytes, cw_off, s));
-  }
-  if (prefixes.empty()) {
-    root_seeds = cwd + cw_off[3];
-    root_cb = reinterpret_cast<uint8_t*>(cwd + cw_off[4]);
-  }
+  DeviceBuffer cws, ccl, ccr;
+  DPF_RETURN_IF_ERROR(cws.Upload(cw.seeds.data(), 16 * levels, s));
+  DPF_RETURN_IF_ERROR(ccl.Upload(cw.ccl.data(), levels, s));
+  DPF_RETURN_IF_ERROR(ccr.Upload(cw.ccr.data(), levels, s));
   const int64_t num_roots = prefixes.empty() ? 1 : num_unique;
   const int64_t expanded = (num_roots << levels) * cepb;
   const size_t stride = static_cast<size_t>(vt.out_stride);
@@ -1998,12 +1970,9 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   }
   DPF_RETURN_IF_ERROR(ClearPadding(vt, expand_out, expanded * stride, s));
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd_expand_and_correct(
-      num_roots, root_seeds, root_cb, levels, cwd + cw_off[0],
-      reinterpret_cast<const uint8_t*>(cwd + cw_off[1]),
-      reinterpret_cast<const uint8_t*>(cwd + cw_off[2]), &vt,
-      reinterpret_cast<const uint64_t*>(corr.data()), ctx.key().party(), cepb, 0,
-      num_roots << levels, expand_out, s)));
-  if (cw_placed) DPF_RETURN_IF_ERROR(ThreadUploadRing().ReleasePlaced(cw_slot, s));
+      num_roots, root_seeds, root_cb, levels, cws.get(), ccl.as<uint8_t>(),
+      ccr.as<uint8_t>(), &vt, reinterpret_cast<const uint64_t*>(corr.data()),
+      ctx.key().party(), cepb, 0, num_roots << levels, expand_out, s)));
 
   trace.Mark("expand_launch");
   void* final_dev = expand_out;

@@ -583,12 +583,35 @@ __device__ __forceinline__ uint32_t Xor3(uint32_t a, uint32_t b, uint32_t c) {
 // the next DPF steps' records (8 each) in flight at P = 2
 constexpr int M4DualPrefetch(int P) { return P == 2 ? DPF_SCAN_M4_DUAL_PF : 1; }
 
+// LDS / VALU query split of the P = 1 pass (A/B experiment, DESIGN.md §3.5,
+// default 0 = off): with more than 48 queries in the pass, the queries of
+// the fourth lane group (48-63) take no table rows — that group's
+// ds_read_b128 work leaves the LDS — and are summed on the VALU instead, in
+// the lane = dword layout the records arrive in: accm[j] ^= x_i & mask, the
+// mask from query 48 + j's selection byte (v_readlane from its lane).
+#ifndef DPF_SCAN_M4_VALU_Q
+#define DPF_SCAN_M4_VALU_Q 0
+#endif
+static_assert(DPF_SCAN_M4_VALU_Q == 0 || DPF_SCAN_M4_VALU_Q == 16, "VALU queries: 0 or 16");
+#ifndef DPF_SCAN_M4_VALU_MASK
+#define DPF_SCAN_M4_VALU_MASK 0  // 1: the per-record masks computed on the VALU
+#endif
+constexpr int kM4ValuQ = DPF_SCAN_M4_VALU_Q;
+constexpr int kM4TableQ = 64 - kM4ValuQ;
+// lanes of the fourth group (upper half, lanes 4-11 / 16-19 / 28-31) in
+// query order (M4LaneMap<1> with SKIP_IDLE): query 48 + j sits in lane
+// kM4Group3Lane[j]
+__device__ __forceinline__ int M4Group3Lane(int j) {
+  return 32 + (j < 8 ? 4 + j : j < 12 ? 16 + (j - 8) : 28 + (j - 12));
+}
+
 template <int P>
 __device__ __forceinline__ void ScanM4Tile2(uint4 s, __amdgpu_buffer_rsrc_t rs,
                                             __amdgpu_buffer_rsrc_t rn, int voff, int rec_bytes,
                                             bool col_ok, uint32_t (&xq)[8 * M4DualPrefetch(P)],
                                             uint32_t (&acc)[64 / P], uint32_t* t, int cpart,
-                                            bool q_ok) {
+                                            bool q_ok, uint32_t (&accm)[kM4ValuQ > 0 ? kM4ValuQ : 1],
+                                            bool valu_pass) {
   constexpr int CPL = 16 / P;
   constexpr int ROW = 17;
   constexpr int DPF = M4DualPrefetch(P);
@@ -613,6 +636,23 @@ __device__ __forceinline__ void ScanM4Tile2(uint4 s, __amdgpu_buffer_rsrc_t rs,
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if constexpr (P == 1 && kM4ValuQ > 0) {
+      if (valu_pass) {  // wave-uniform: queries 48-63 on the VALU, every lane
+#pragma unroll
+        for (int j = 0; j < kM4ValuQ; ++j) {
+          uint32_t sbj = __builtin_amdgcn_readlane(sb, M4Group3Lane(j));
+#if DPF_SCAN_M4_VALU_MASK
+          // the masks on the VALU (the scalar unit is shared by the CU's SIMDs)
+          asm volatile("v_mov_b32 %0, %1" : "=v"(sbj) : "s"(sbj));
+#endif
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const uint32_t m = 0u - ((sbj >> i) & 1u);
+            accm[j] = __builtin_amdgcn_bitop3_b32(accm[j], i < 4 ? xa[i] : xb[i - 4], m, 0x78);
+          }
+        }
+      }
+    }
     // groups 2k and 2k + 1: low nibble for table A
     if (P == 1 && DPF_SCAN_M4_SKIP_IDLE && !q_ok) return;  // an idle lane reads nothing
     const uint4* ra = reinterpret_cast<const uint4*>(t) + (sb & 15) * ROW + cpart * CPL;
@@ -717,6 +757,13 @@ void KPirScanM4(ScanArgs a) {
   const int width = min(64, a.C * 4 - dw_lo);  // dwords of this slice
   const bool col_ok = lane < width;
   const bool q_ok = q < a.nq;
+  // the VALU split (P = 1, more than 48 queries): lanes of queries 48-63
+  // load their selection blocks (read by v_readlane) but take no table rows
+  const bool valu_pass = P == 1 && DUAL && kM4ValuQ > 0 && a.nq > kM4TableQ;
+  const bool q_tab = q_ok && !(valu_pass && ql >= kM4TableQ);
+  uint32_t accm[kM4ValuQ > 0 ? kM4ValuQ : 1];
+#pragma unroll
+  for (int j = 0; j < (kM4ValuQ > 0 ? kM4ValuQ : 1); ++j) accm[j] = 0u;
   uint32_t* t = reinterpret_cast<uint32_t*>(tab[wave]);
   t[lane] = 0u;  // row 0 (no record selected) stays zero
   if (TABLES == 2) t[16 * ROW * 4 + lane] = 0u;
@@ -743,7 +790,8 @@ void KPirScanM4(ScanArgs a) {
       const uint4 sn = (q_ok && more) ? a.sel[(int64_t)(a.q0 + q) * a.sel_blocks + next]
                                       : make_uint4(0, 0, 0, 0);
       if constexpr (DUAL)
-        ScanM4Tile2<P>(s, rs, rn, voff, rec_bytes, col_ok, xq, acc, t, cpart, q_ok);
+        ScanM4Tile2<P>(s, rs, rn, voff, rec_bytes, col_ok, xq, acc, t, cpart, q_tab, accm,
+                       valu_pass);
       else
         ScanM4Tile<P>(s, rs, rn, voff, rec_bytes, col_ok, xq, acc, t, lane, cpart);
       if (!more) break;
@@ -752,7 +800,16 @@ void KPirScanM4(ScanArgs a) {
       s = sn;
     }
   }
-  if (!q_ok) return;
+  if constexpr (P == 1 && kM4ValuQ > 0) {
+    if (valu_pass) {  // dword `lane` of the slice of each VALU query
+      for (int j = 0; j < kM4ValuQ && kM4TableQ + j < a.nq; ++j) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(
+            a.partials + (part * a.total_q + a.q0 + kM4TableQ + j) * a.C + blockIdx.y * 16);
+        if (col_ok) o[lane] = accm[j];
+      }
+    }
+  }
+  if (!q_tab) return;
   // this lane's columns [cpart * CPL, +CPL) of the slice, clipped to the record
   uint4* out = a.partials + (part * a.total_q + a.q0 + q) * a.C + blockIdx.y * 16;
   const int chunks = (width + 3) / 4;

@@ -397,6 +397,8 @@ SCAN_CASES = [(1, 16, 1), (1000, 256, 1), (1000, 256, 3), (4096, 80, 8), (300, 1
               # narrow last slice (1104 B = 4 x 256 + 80), 100 queries
               (1000, 256, 17), (3001, 256, 32), (4097, 512, 33), (130, 256, 64),
               (2500, 768, 100), (2049, 1104, 40), (640, 240, 16), (385, 64, 9),
+              # 49-64 queries in one P = 1 pass (the fourth lane group in use)
+              (3001, 256, 49), (2049, 1104, 57),
               # 9-15 queries: the Four-Russians scan from 9 on (P = 4)
               (3000, 256, 12), (2001, 1104, 15), (1500, 256, 10),
               # >= 64 scan blocks with a partial of <= 2 KiB: the masked scan
