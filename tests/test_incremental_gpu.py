@@ -83,12 +83,27 @@ def expand_mode(request, api):
     L.dpf_amd_set_prefix_expand(prev)
 
 
-@pytest.mark.parametrize("single_point", [False, True])
+# (single_point, EvaluateUntil strategy): EvaluateAt does not expand, so it
+# runs once, under the default strategy
+CALL_MODES = [(False, 0), (False, 1), (False, 2), (True, 0)]
+
+
+@pytest.mark.parametrize("single_point,mode", CALL_MODES,
+                         ids=["until-prefix_expand", "until-unique_expand_gather",
+                              "until-host_bookkeeping", "at"])
 @pytest.mark.parametrize("suite", IC.SUITES, ids=[s[0] for s in IC.SUITES])
-def test_incremental_dpf_correctness_vs_oracle(api, suite, single_point, expand_mode):
+def test_incremental_dpf_correctness_vs_oracle(api, suite, single_point, mode):
+    from distributed_point_functions_amd import _lib
+    L = _lib.lib()
+    prev = L.dpf_amd_set_prefix_expand(mode)
+    try:
+        _incremental_suite(api, suite, single_point)
+    finally:
+        L.dpf_amd_set_prefix_expand(prev)
+
+
+def _incremental_suite(api, suite, single_point):
     name, hier, alphas, betas_list, steps = suite
-    if single_point and expand_mode:
-        pytest.skip("EvaluateAt does not expand")
     levels = IC.levels_of(hier)
     dpf = _make(api, levels)
     od = po.Dpf(levels)
