@@ -214,7 +214,9 @@ static int EvaluateUntilImpl(const dpf_amd_dpf* dpf, int hierarchy_level,
                       ? hierarchy_level
                       : 0;
   const dpf_amd_value_type layout = dpf->dpf->value_type_descriptor(lvl);
-  const int64_t cap = layout.out_stride > 0 ? out_capacity / layout.out_stride : 0;
+  // (a negative capacity passes through: the unvalidated size query)
+  const int64_t cap = out_capacity < 0 ? -1
+                      : layout.out_stride > 0 ? out_capacity / layout.out_stride : 0;
   st = dpf->dpf->EvaluateUntilRaw(hierarchy_level, Span<const uint128>(p.data(), p.size()),
                                   ctx->ctx, layout, out, cap, num_outputs, out_on_device, stream);
   return st.ok() ? DPF_AMD_OK : Fail(st);

@@ -1711,7 +1711,11 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
                                     " out of range for hierarchy level " + std::to_string(prev_h));
     return OkStatus();
   };
-  // (a size query, out == nullptr, runs the serial check before it answers)
+  // (a size query, out == nullptr, runs the serial check before it answers
+  // unless out_capacity < 0: the two-call protocol's first call, whose
+  // evaluation call validates the same prefixes right after — the C++
+  // header template and the Python mirror)
+  const bool size_unchecked = out == nullptr && out_capacity < 0;
   const bool range_deferred =
       out == nullptr || static_cast<int64_t>(prefixes.size()) >= (int64_t{1} << 14);
   if (!range_deferred) DPF_RETURN_IF_ERROR(range_check());
@@ -1729,7 +1733,7 @@ Status DistributedPointFunction::EvaluateUntilRaw(int hierarchy_level,
   const int64_t outputs_per_prefix = int64_t{1} << (log_domain_size - previous_log_domain_size);
   const int64_t total = prefixes.empty() ? outputs_per_prefix : num_prefixes * outputs_per_prefix;
   *num_outputs = total;
-  if (out == nullptr) return early(OkStatus());
+  if (out == nullptr) return size_unchecked ? OkStatus() : early(OkStatus());
   if (out_capacity < total) return early(InvalidArgumentError("output buffer too small"));
 
   const LevelMeta& m = st.levels[hierarchy_level];

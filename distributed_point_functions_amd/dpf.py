@@ -267,8 +267,9 @@ class DistributedPointFunction:
         n = ctypes.c_int64()
         L = _lib.lib()
         pp = pw.ctypes.data_as(ctypes.c_void_p)
+        # size only; the evaluation call below validates the prefixes
         check(L.dpf_amd_evaluate_until(self._h, hierarchy_level, pp, len(prefixes), tp, len(tp),
-                                       ctx._h, None, 0, ctypes.byref(n)))
+                                       ctx._h, None, -1, ctypes.byref(n)))
         if out is not None:
             check(L.dpf_amd_evaluate_until_device(
                 self._h, hierarchy_level, pp, len(prefixes), tp, len(tp), ctx._h,

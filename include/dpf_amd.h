@@ -393,7 +393,10 @@ int64_t dpf_amd_ctx_num_partial_evaluations(const dpf_amd_ctx* ctx);
  * ValueType of T (checked as in h:709-716).  Writes host-layout T values to
  * `out` (capacity in bytes); *num_outputs receives the element count.  With
  * out == NULL only *num_outputs is computed, after the same validation as an
- * evaluation (arguments, context, and every prefix in range, h:735-745). */
+ * evaluation (arguments, context, and every prefix in range, h:735-745);
+ * with out == NULL and out_capacity < 0 the prefixes' range check is left
+ * to the evaluation call that follows (the two-call protocol's first call:
+ * one pass over a long prefix list instead of two). */
 int dpf_amd_evaluate_until(const dpf_amd_dpf* dpf, int hierarchy_level,
                            const uint64_t* prefixes, int64_t num_prefixes,
                            const uint8_t* value_type, size_t value_type_len,

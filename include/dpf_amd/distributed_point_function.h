@@ -128,8 +128,9 @@ class DistributedPointFunction {
                                          EvaluationContext& ctx) const {
     DPF_RETURN_IF_ERROR(CheckType(ToValueType<T>(), hierarchy_level, false));
     int64_t n = 0;
+    // size only (capacity -1: the prefixes are validated by the call below)
     DPF_RETURN_IF_ERROR(EvaluateUntilRaw(hierarchy_level, prefixes, ctx, LayoutOf<T>(),
-                                         nullptr, 0, &n, false, nullptr));
+                                         nullptr, -1, &n, false, nullptr));
     std::vector<T> out(n);
     DPF_RETURN_IF_ERROR(EvaluateUntilRaw(hierarchy_level, prefixes, ctx, LayoutOf<T>(),
                                          out.data(), n, &n, false, nullptr));

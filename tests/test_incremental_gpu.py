@@ -328,7 +328,8 @@ def test_context_outlives_the_callers_stream(api):
 def test_size_query_validates_prefixes(api):
     """dpf_amd_evaluate_until with out == NULL (the size query) rejects a
     prefix outside the previous level's domain with the reference's error
-    (h:735-745), for short and for long prefix lists."""
+    (h:735-745), for short and for long prefix lists; with a negative
+    capacity it only counts, and the evaluation reports the error."""
     import ctypes
     from distributed_point_functions_amd import _lib
     D, V = api
@@ -347,6 +348,13 @@ def test_size_query_validates_prefixes(api):
         assert rc == 3
         msg = L.dpf_amd_last_error().decode()
         assert "Index %d out of range for hierarchy level 0" % max(pre) in msg, msg
+        # capacity < 0: the two-call protocol's size-only query leaves the
+        # range check to the evaluation call
+        assert L.dpf_amd_evaluate_until(dpf._h, 1, pw.ctypes.data_as(ctypes.c_void_p), len(pre),
+                                        tp, len(tp), ctx._h, None, -1, ctypes.byref(n)) == 0
+        assert n.value == len(pre) * 256
+        with pytest.raises(Exception, match="out of range for hierarchy level 0"):
+            dpf.evaluate_until(1, pre, ctx)
         # in range: the size query answers
         ok = [p for p in pre if p < 256][:50]
         pw = po.u128_words(ok)
