@@ -252,6 +252,27 @@ __device__ __forceinline__ void FoldPartials(const ScanArgs& a, const uint4 (&ac
 #ifndef DPF_SCAN_G1_XCD
 #define DPF_SCAN_G1_XCD 1
 #endif
+// Four-Russians kernels over records wider than one 256-byte slice: the same
+// slice-major, XCD-local block order (A/B: DPF_SCAN_M4_SLICE_MAJOR).
+#ifndef DPF_SCAN_M4_SLICE_MAJOR
+#define DPF_SCAN_M4_SLICE_MAJOR 0
+#endif
+// (part block, slice) of this block: a 1-D grid of blocks x slices when the
+// launch is slice-major (ScanArgs::slice_major), else (blockIdx.x, blockIdx.y).
+__device__ __forceinline__ void M4BlockSlice(const ScanArgs& a, int64_t& pb, int& slice) {
+  if (!a.slice_major) {
+    pb = blockIdx.x;
+    slice = blockIdx.y;
+    return;
+  }
+  const int slices = (a.C + 15) / 16;
+  int64_t lb = blockIdx.x;
+  const int64_t full = gridDim.x & ~7u;
+  if (lb < full) lb = (lb & 7) * (full >> 3) + (lb >> 3);
+  pb = lb / slices;
+  slice = (int)(lb % slices);
+}
+
 template <int QN, int G>
 __global__ __launch_bounds__(kScanBlock) void KPirScanG(ScanArgs a) {
   constexpr int U = (G >= 64) ? 2 : (G == 1) ? DPF_SCAN_G1_U : (G * 8 <= 32) ? 8 : 32 / G;
@@ -776,12 +797,15 @@ void KPirScanM4(ScanArgs a) {
   // pass over the rows instead of two, no barrier (the pair's second loads
   // of a tile mostly hit in cache).
   const int qg = a.qgroups;
-  const int64_t part = (int64_t)blockIdx.x * (kScanM4Waves / qg) + wave / qg;
+  int64_t pb;
+  int slice;
+  M4BlockSlice(a, pb, slice);
+  const int64_t part = pb * (kScanM4Waves / qg) + wave / qg;
   if (part >= a.parts) return;  // wave-uniform; no block barrier below
   int ql, cpart;
   M4LaneMap<P>(lane, ql, cpart);
   const int q = (wave % qg) * QW + ql;
-  const int dw_lo = blockIdx.y * 64;
+  const int dw_lo = slice * 64;
   const int width = min(64, a.C * 4 - dw_lo);  // dwords of this slice
   const bool col_ok = lane < width;
   const bool q_ok = q < a.nq;
@@ -832,14 +856,14 @@ void KPirScanM4(ScanArgs a) {
     if (valu_pass) {  // dword `lane` of the slice of each VALU query
       for (int j = 0; j < kM4ValuQ && kM4TableQ + j < a.nq; ++j) {
         uint32_t* o = reinterpret_cast<uint32_t*>(
-            a.partials + (part * a.total_q + a.q0 + kM4TableQ + j) * a.C + blockIdx.y * 16);
+            a.partials + (part * a.total_q + a.q0 + kM4TableQ + j) * a.C + slice * 16);
         if (col_ok) o[lane] = accm[j];
       }
     }
   }
   if (!q_tab) return;
   // this lane's columns [cpart * CPL, +CPL) of the slice, clipped to the record
-  uint4* out = a.partials + (part * a.total_q + a.q0 + q) * a.C + blockIdx.y * 16;
+  uint4* out = a.partials + (part * a.total_q + a.q0 + q) * a.C + slice * 16;
   const int chunks = (width + 3) / 4;
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
@@ -904,11 +928,13 @@ void KPirScanM4Pair(ScanArgs a) {
   __shared__ uint4 tab[2][2][16 * ROW];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t part = blockIdx.x;  // block-uniform: both waves take the barriers
+  int64_t part;  // block-uniform: both waves take the barriers
+  int slice;
+  M4BlockSlice(a, part, slice);
   int ql, cpart;
   M4LaneMap<1>(lane, ql, cpart);  // queries fill whole lane groups (idle groups skip reads)
   const int q = wave * 64 + ql;
-  const int dw_lo = blockIdx.y * 64;
+  const int dw_lo = slice * 64;
   const int width = min(64, a.C * 4 - dw_lo);
   const bool col_ok = lane < width;
   const bool q_ok = q < a.nq;
@@ -954,7 +980,7 @@ void KPirScanM4Pair(ScanArgs a) {
     }
   }
   if (!q_ok) return;
-  uint4* out = a.partials + (part * a.total_q + a.q0 + q) * a.C + blockIdx.y * 16;
+  uint4* out = a.partials + (part * a.total_q + a.q0 + q) * a.C + slice * 16;
   const int chunks = (width + 3) / 4;
 #pragma unroll
   for (int c = 0; c < 16; ++c)
@@ -973,10 +999,13 @@ int LaunchPirScanM4(int nq, int parts, int slices, hipStream_t st, const ScanArg
   const int P = nq > 32 ? 1 : nq > 16 ? 2 : 4;
   ScanArgs a = args;
   a.qgroups = nq > 64 ? 2 : 1;
+  a.slice_major = (DPF_SCAN_M4_SLICE_MAJOR && slices > 1) ? 1 : 0;
   const int per_block = kScanM4Waves / a.qgroups;
-  const dim3 g((parts + per_block - 1) / per_block, slices);
+  const dim3 g = a.slice_major ? dim3(((parts + per_block - 1) / per_block) * slices, 1)
+                               : dim3((parts + per_block - 1) / per_block, slices);
   if (DPF_SCAN_M4_SHARED && a.qgroups == 2) {
-    hipLaunchKernelGGL(KPirScanM4Pair, dim3(parts, slices), dim3(kScanM4PairBlock), 0, st, a);
+    const dim3 gp = a.slice_major ? dim3(parts * slices, 1) : dim3(parts, slices);
+    hipLaunchKernelGGL(KPirScanM4Pair, gp, dim3(kScanM4PairBlock), 0, st, a);
   } else if (P == 1)
     hipLaunchKernelGGL((KPirScanM4<1>), g, dim3(kScanM4Block), 0, st, a);
   else if (P == 2)

@@ -156,6 +156,9 @@ struct ScanArgs {
   // is not read, as the reference's scan skips it (inner_product_hwy.cc:
   // 213-221) — the access pattern then follows the selection share.
   int32_t skip;
+  // KPirScanM4*: 1 = a 1-D grid of (part block, 256-byte slice) pairs,
+  // slice-major and XCD-local (set by LaunchPirScanM4)
+  int32_t slice_major;
 };
 
 // Fold slots of the masked scan when a pass's partial is small: 64 slots,

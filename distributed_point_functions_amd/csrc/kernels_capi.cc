@@ -570,6 +570,9 @@ int dpf_amd_evaluate_points_batched(int64_t num_keys, int64_t points_per_key,
 
 }  // extern "C"
 
+#ifndef DPF_SCAN_GRID_WIDE
+#define DPF_SCAN_GRID_WIDE 0
+#endif
 static int ScanGrid(int64_t num_records, int num_queries, int64_t record_stride) {
   // At least one 128-record tile per wave; up to 8192 blocks / partials
   // (c4 Q = 8: 2.95 ms vs 3.17 ms at 2048 — more, shorter blocks balance
@@ -579,7 +582,13 @@ static int ScanGrid(int64_t num_records, int num_queries, int64_t record_stride)
   const int64_t tiles = (num_records + 127) / 128;
   const int64_t g = (tiles + kScanWaves - 1) / kScanWaves;
   const int64_t per_block = std::max<int64_t>(1, (int64_t)num_queries * record_stride);
-  const int64_t cap = std::max<int64_t>(2048, std::min<int64_t>(8192, (256ll << 20) / per_block));
+  // Rows wider than one masked-scan slice (64 chunks) multiply the blocks by
+  // their slices, so the floor that keeps the CUs busy divides by them
+  // (DPF_SCAN_GRID_WIDE; A/B): 16 KiB rows at Q = 100 write 0.4 GB of
+  // partials instead of 3.4 GB.
+  const int64_t slices = DPF_SCAN_GRID_WIDE ? std::max<int64_t>(1, (record_stride / 16 + 63) / 64) : 1;
+  const int64_t floor = std::max<int64_t>(256, 2048 / slices);
+  const int64_t cap = std::max<int64_t>(floor, std::min<int64_t>(8192, (256ll << 20) / per_block));
   return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
 }
 
@@ -660,6 +669,7 @@ int ScanPiece(const void* db, int64_t num_records, int64_t record_stride,
   a.qgroups = 1;
   a.slots = plan.slots ? kScanSlots : 0;
   a.skip = t_scan_skip;
+  a.slice_major = 0;
   const dim3 g(grid, (C + 63) / 64);
   for (int q0 = 0; q0 < num_queries;) {
     const int rem = num_queries - q0;

@@ -4,6 +4,7 @@ at run time with DPF_AMD_LIB=<path>).  The other objects are the main build's.
 
     python tools/build_variants.py k_expand_c5.hip name1:DEF=1,DEF2=3 name2:...
     python tools/build_variants.py all name:DEF=1     # every .hip TU
+    python tools/build_variants.py k_pir.hip+kernels_capi.cc name:DEF=1
 """
 import concurrent.futures
 import os
@@ -16,10 +17,11 @@ from distributed_point_functions_amd import build_native as B  # noqa: E402
 
 
 def main():
-    tu = sys.argv[1]
+    tu = sys.argv[1]  # one unit, several joined by "+", or "all" (every .hip unit)
+    tus = tu.split("+")
     B.build()
     objs = [os.path.join(B.OBJ_DIR, os.path.basename(s) + ".o") for s in B._sources()]
-    others = [o for o in objs if os.path.basename(o) != tu + ".o"]
+    others = [o for o in objs if os.path.basename(o)[:-2] not in tus]
 
     def one(spec):
         name, _, defs = spec.partition(":")
@@ -31,7 +33,7 @@ def main():
             rest = [o for o in objs if not o.endswith(".hip.o")]
             parts = mine + rest
         else:
-            parts = [B._compile(os.path.join(B.CSRC, tu), True, d, dl)] + others
+            parts = [B._compile(os.path.join(B.CSRC, t), True, d, dl) for t in tus] + others
         lib = os.path.join(d, "libdpf_amd.so")
         subprocess.check_call(["hipcc", "--offload-arch=" + B.ARCH, "-shared", "-fPIC", "-o", lib] +
                               parts + ["-lpthread"])
