@@ -253,9 +253,13 @@ __device__ __forceinline__ void FoldPartials(const ScanArgs& a, const uint4 (&ac
 #define DPF_SCAN_G1_XCD 1
 #endif
 // Four-Russians kernels over records wider than one 256-byte slice: the same
-// slice-major, XCD-local block order (A/B: DPF_SCAN_M4_SLICE_MAJOR).
+// slice-major, XCD-local block order.  With the wide-row grid sizing
+// (kernels_capi.cc ScanGrid), alternated (profiles/ab_scan_wide_r06k/):
+// 2^20 x 2 KiB Q = 10 / 100 0.64 / 1.12 -> 0.53 / 1.00 ms, 16 KiB 3.98 /
+// 7.72 -> 3.70 / 6.07 ms (FETCH of the Q = 100 scan 31.7 -> 23.5 GB, its
+// fold 6.7 -> 0.8 GB); c4 unchanged.
 #ifndef DPF_SCAN_M4_SLICE_MAJOR
-#define DPF_SCAN_M4_SLICE_MAJOR 0
+#define DPF_SCAN_M4_SLICE_MAJOR 1
 #endif
 // (part block, slice) of this block: a 1-D grid of blocks x slices when the
 // launch is slice-major (ScanArgs::slice_major), else (blockIdx.x, blockIdx.y).
