@@ -259,8 +259,15 @@ def c3(dev, reps):
         nz = np.nonzero(s)[0]
         ok &= len(nz) == 1 and int(s[nz[0]]) == betas[i]
     leaves = sum(len(x) for x in a)
+    # LDS-lookup fraction of a whole level (device outputs): per prefix the
+    # walk from the stored partial evaluation (8 levels) and to the prefix's
+    # own node (1), then its 2^7-leaf subtree (2 (2^7 - 1) tree + 2^7 value
+    # AES) — 391 AES x 160 lookups, over the level's wall time
+    lvl = [len(prefixes[i]) * 391 * 160 / best["device"][i] / LDS_PEAK_LOOKUPS
+           for i in range(2, H)]
     return {"config": "c3", "workload": "heavy hitters, 16 levels x 8 bits, uint64, 2^16 prefixes",
             "returned_leaves": leaves,
+            "level_lds_frac_median": float(np.median(lvl)),
             "host_out_ms_total": 1e3 * sum(best["host"]),
             "host_out_ms_per_level": [round(1e3 * t, 3) for t in best["host"]],
             "host_out_leaves_per_s": leaves / sum(best["host"]),
