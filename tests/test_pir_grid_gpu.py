@@ -10,8 +10,9 @@ words, the KPirScanG G = 1 slices and KPirScanM4's row staging) run at the
 grid's record count with a ragged last tile (2^20 - 45 records: the last
 128-record selection block is partial, and its bits past the end are set),
 built through the bulk variable-size insert (dpf_amd_pir_db_insert_packed,
-Builder::Insert per record).  Selections are random inside three 4,096-record
-windows (the first, one in the middle, the last reaching the ragged end) and
+Builder::Insert per record), stored at whole 128-byte lines per row.
+Selections are random inside three 4,096-record windows (the first, one in
+the middle, the last reaching the ragged end) and
 zero elsewhere, so the oracle (inner_product_hwy.cc:270-296) checks the
 windows' records while the scan streams the whole table; records outside the
 windows are a non-periodic pattern, so a row leaking into a sum would show.
@@ -59,13 +60,23 @@ def grid_db(request, cuda):
     torch.cuda.empty_cache()
 
 
+def device_row_stride(max_size):
+    """The database's row stride (csrc/pir.cc DeviceRowStride): the
+    reference's 16-byte alignment (dense_dpf_pir_database.cc:40-52), padded
+    to whole 128-byte lines when that costs at most 1/16 more bytes."""
+    s16 = max(16, (max_size + 15) // 16 * 16)
+    s128 = (s16 + 127) // 128 * 128
+    return s128 if (s128 - s16) * 16 <= s16 else s16
+
+
 def test_grid_database_layout(grid_db):
-    """Rows at the reference's 16-byte alignment of the largest value
-    (dense_dpf_pir_database.cc:40-52, 112-153); results as long as it."""
+    """Wide rows start on a cache line; results are as long as the largest
+    value (inner_product_hwy.cc:252-256)."""
     db, sizes = grid_db["db"], grid_db["sizes"]
     assert db.size == N
     assert db.max_value_size == int(sizes.max())
-    assert db.record_stride == (int(sizes.max()) + 15) // 16 * 16
+    assert db.record_stride == device_row_stride(int(sizes.max()))
+    assert db.record_stride % 128 == 0
 
 
 @pytest.mark.parametrize("q", [1, 2, 10, 100])

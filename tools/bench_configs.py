@@ -316,6 +316,7 @@ def c4q(dev, reps):
 GRID_AVGS = (32, 256, 2048, 16384)
 GRID_NS = (1 << 16, 1 << 20)
 GRID_QS = (1, 2, 10, 100)
+GRID_ALIGN = 0
 
 
 def pirgrid(dev, reps):
@@ -333,7 +334,14 @@ def pirgrid(dev, reps):
     gen.manual_seed(125)
     rows = []
     for avg in GRID_AVGS:
-        rec = (avg + 7 + 15) // 16 * 16  # AlignBytes of the largest value
+        # the database's row stride for the largest value (pir.cc
+        # DeviceRowStride: 16-byte aligned, whole 128-byte lines when that
+        # costs at most 1/16 more), or a forced alignment (layout A/B)
+        rec = (avg + 7 + 15) // 16 * 16
+        if GRID_ALIGN > 16:
+            rec = (rec + GRID_ALIGN - 1) // GRID_ALIGN * GRID_ALIGN
+        elif GRID_ALIGN == 0 and ((rec + 127) // 128 * 128 - rec) * 16 <= rec:
+            rec = (rec + 127) // 128 * 128
         for n in GRID_NS:
             db_t = torch.randint(0, 256, (n * rec,), dtype=torch.uint8, device=dev, generator=gen)
             db = P.DenseDpfPirDatabase()
@@ -562,10 +570,14 @@ def main():
     ap.add_argument("--c4q-queries", default=None, help="comma list, e.g. 64 (profiling)")
     ap.add_argument("--no-ab", action="store_true", help="c4q: skip the kernel A/B")
     ap.add_argument("--c2-batched-only", action="store_true", help="c2: the batched kernel only")
+    ap.add_argument("--grid-align", type=int, default=0,
+                    help="pirgrid: row stride rounded up to this many bytes (layout A/B; "
+                         "0: the database's own rule)")
     ap.add_argument("--grid", default=None,
                     help="pirgrid subset as avg:n:q lists, e.g. 16384:1048576:1 (profiling)")
     args = ap.parse_args()
-    global C4Q_QUERIES, C4Q_AB, C2_BATCHED_ONLY, GRID_AVGS, GRID_NS, GRID_QS
+    global C4Q_QUERIES, C4Q_AB, C2_BATCHED_ONLY, GRID_AVGS, GRID_NS, GRID_QS, GRID_ALIGN
+    GRID_ALIGN = args.grid_align
     if args.grid:
         a, n, q = args.grid.split(":")
         GRID_AVGS = tuple(int(x) for x in a.split(","))
