@@ -11,6 +11,10 @@
 #endif
 #include "aes_device.h"
 
+#ifndef DPF_EXPAND_EXTRA_DEPTHS
+#define DPF_EXPAND_EXTRA_DEPTHS 0  // KExpand<3>, <5> for A/B builds
+#endif
+
 #ifndef DPF_EXPAND_MAX_GRID
 #define DPF_EXPAND_MAX_GRID (1 << 24)
 #endif
@@ -245,6 +249,42 @@ constexpr bool kStaged = kStagedEm<Em> && (1 << D) >= DPF_STAGE_LEAVES;
 
 // Leaf j of the lane's subtree (j wave-uniform): staged when the emitter
 // writes packed 16-byte leaves, flushed as one burst per DPF_STAGE_LEAVES.
+// Progress-ordered wave priority (A/B: DPF_EXPAND_PRIO=1).  The sequencer
+// favours older waves, so within a round of resident blocks the oldest waves
+// run ahead and finish first, and the last ones run alone at an occupancy
+// too low to keep the LDS busy.  A wave starts at priority 3 and steps down
+// one level per quarter of its subtree's leaves, so waves that are behind
+// are served first and a round's waves finish together.
+#ifndef DPF_EXPAND_PRIO
+#define DPF_EXPAND_PRIO 0
+#endif
+template <int D>
+__device__ __forceinline__ void ProgressPrio(int j) {
+  if constexpr (DPF_EXPAND_PRIO == 2 && D >= 2) {
+    // geometric: priority 3 up to 3/4 of the leaves, 2 to 7/8, 1 to 15/16
+    // (D = 2: 3/4 only), so the final spread is at most 1/16 of the work
+    const int done = j + 1;
+    constexpr int n = 1 << D;
+    if (done == n - n / 4)
+      __builtin_amdgcn_s_setprio(2);
+    else if (D >= 3 && done == n - n / 8)
+      __builtin_amdgcn_s_setprio(1);
+    else if (D >= 4 && done == n - n / 16)
+      __builtin_amdgcn_s_setprio(0);
+  } else if constexpr (DPF_EXPAND_PRIO == 1 && D >= 2) {
+    const int done = j + 1;  // leaves emitted (wave-uniform)
+    if ((done & ((1 << (D - 2)) - 1)) == 0) {
+      const int q = done >> (D - 2);  // quarters done, 1..4
+      if (q == 1)
+        __builtin_amdgcn_s_setprio(2);
+      else if (q == 2)
+        __builtin_amdgcn_s_setprio(1);
+      else if (q == 3)
+        __builtin_amdgcn_s_setprio(0);
+    }
+  }
+}
+
 template <int D, class Em, int BN>
 __device__ __forceinline__ void EmitStagedLeaf(const ExpandCtx& E, LeafStage& S,
                                          const uint32_t (&h)[BN][4], uint32_t t,
@@ -268,10 +308,12 @@ __device__ __forceinline__ void EmitStagedLeaf(const ExpandCtx& E, LeafStage& S,
           for (int i = 0; i < N; ++i) StoreLeaf16(E, S.v[i], g0 + i);
         }
       }
+      ProgressPrio<D>(j);
       return;
     }
   }
   Em::Emit(E, h, t, (chunk << D) + j);
+  ProgressPrio<D>(j);
 }
 
 template <int DEPTH, int D, class Em>
@@ -316,11 +358,39 @@ __device__ __forceinline__ void Dfs(const ExpandCtx& E, LeafStage& S, const uint
 // Batched keys (kBatched, ExpandArgs::batched): lane i's chunk id maps to
 // key id / (chunk_end - chunk_begin) with that key's root, correction words,
 // value correction and party; leaf ranges and outputs are per key.
+// Per-wave timestamps of KExpand (diagnostic builds only: tools/expand_trace.py
+// builds one translation unit with DPF_EXPAND_TRACE=1): per wave, lane 0's
+// s_memrealtime (100 MHz) at entry, after the tables, after the walk and at
+// the end (slots 0-3), s_memtime (shader clock) at entry and end (4-5), and
+// the HW_ID / XCC_ID registers (6-7).
+#if DPF_EXPAND_TRACE
+__device__ uint64_t g_expand_trace[16384 * 8];
+extern "C" __attribute__((visibility("default"))) int dpf_amd_debug_expand_trace(void* host,
+                                                                                 int64_t bytes) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_expand_trace), (size_t)bytes, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#define DPF_EXP_MARK(i, v)                                                          \
+  do {                                                                              \
+    const int w_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);             \
+    if ((threadIdx.x & 63) == 0 && w_ < 16384) g_expand_trace[w_ * 8 + (i)] = (v); \
+  } while (0)
+#else
+#define DPF_EXP_MARK(i, v) \
+  do {                     \
+  } while (0)
+#endif
+
 template <int D, class Em, bool kBatched = false>
 __global__ __launch_bounds__(kBlockOf<Em>, kWavesOf<Em>) void KExpand(ExpandArgs a, VtDev vt) {
   __shared__ uint32_t tab[kTabWords];
+  DPF_EXP_MARK(0, __builtin_amdgcn_s_memrealtime());
+  DPF_EXP_MARK(4, __builtin_amdgcn_s_memtime());
+  DPF_EXP_MARK(6, (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4));
+  DPF_EXP_MARK(7, (uint64_t)__builtin_amdgcn_s_getreg((3 << 11) | 20));
   FillTables(tab);
   __syncthreads();
+  DPF_EXP_MARK(1, __builtin_amdgcn_s_memrealtime());
   const Lds L = MakeLds(tab);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t cpk = a.chunk_end - a.chunk_begin;
@@ -328,6 +398,7 @@ __global__ __launch_bounds__(kBlockOf<Em>, kWavesOf<Em>) void KExpand(ExpandArgs
   // Every lane runs the same number of iterations (uniform trip count), so
   // the per-level wave votes below see all lanes; lanes past the end idle.
   for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < total; base += stride) {
+    if (DPF_EXPAND_PRIO) __builtin_amdgcn_s_setprio(3);
     const int64_t id = base + threadIdx.x;
     const bool live = id < total;
     const int64_t cid = live ? id : total - 1;
@@ -368,6 +439,7 @@ __global__ __launch_bounds__(kBlockOf<Em>, kWavesOf<Em>) void KExpand(ExpandArgs
         t = bit ? tr : tl;
       }
     }
+    DPF_EXP_MARK(2, __builtin_amdgcn_s_memrealtime());
     ExpandArgs ak = a;
     ExpandCtx E{ak, vt, L};
     if constexpr (kBatched) {
@@ -384,6 +456,8 @@ __global__ __launch_bounds__(kBlockOf<Em>, kWavesOf<Em>) void KExpand(ExpandArgs
     LeafStage S;
     if (live) Dfs<D, D, Em>(E, S, x, t, kBatched ? a.walk : a.root_level + a.walk, c, 0);
   }
+  DPF_EXP_MARK(3, __builtin_amdgcn_s_memrealtime());
+  DPF_EXP_MARK(5, __builtin_amdgcn_s_memtime());
 }
 
 template <int D, class Em>
@@ -751,6 +825,12 @@ int LaunchExpandAnyD(int D, int grid, hipStream_t st, const ExpandArgs& a, const
       return LaunchExpand<4, Em>(grid, st, a, vt);
     case 6:
       return LaunchExpand<6, Em>(grid, st, a, vt);
+#if DPF_EXPAND_EXTRA_DEPTHS  // A/B builds only (tools/ab_c3_depth.sh)
+    case 3:
+      return LaunchExpand<3, Em>(grid, st, a, vt);
+    case 5:
+      return LaunchExpand<5, Em>(grid, st, a, vt);
+#endif
     default:
       return LaunchExpand<8, Em>(grid, st, a, vt);
   }

@@ -17,6 +17,12 @@
 #include "kernel_args.h"
 #include "host_device.h"
 
+// D = 3 and 5 for the KExpand depth A/B (tools/ab_c3_depth.sh); the product
+// build instantiates D in {0, 1, 2, 4, 6, 8}.
+#ifndef DPF_EXPAND_EXTRA_DEPTHS
+#define DPF_EXPAND_EXTRA_DEPTHS 0
+#endif
+
 namespace dpf_amd {
 
 namespace {
@@ -444,8 +450,9 @@ int dpf_amd_expand_and_correct_batched(int64_t num_keys, const void* root_seeds,
 }
 
 int dpf_amd_set_expand_depth(int depth) {
+  const bool extra = DPF_EXPAND_EXTRA_DEPTHS && (depth == 3 || depth == 5);
   if (depth != 0 && depth != 1 && depth != 2 && depth != 4 && depth != 6 && depth != 8 &&
-      depth != -1 && depth != -2 && depth != -3)
+      depth != -1 && depth != -2 && depth != -3 && !extra)
     return -99;
   const int old = t_expand_depth;
   t_expand_depth = depth;

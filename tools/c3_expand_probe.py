@@ -2,7 +2,7 @@
 levels below each, uint64 outputs (two per tree leaf), KExpand at the
 automatic depth or a forced one; event-timed, with the LDS-lookup fraction
 (490 lookups per tree leaf at D = 4: 3 walk + 30 tree + 16 value AES per 16
-leaves, 160 each).  Used to see whether the 2^16-root launch (2^19 threads,
+leaves, 160 each; likewise for a forced D).  Used to see whether the 2^16-root launch (2^19 threads,
 1024 blocks = two rounds of 512 slots) loses to its tail.
 
     python tools/c3_expand_probe.py [--roots 15,16,17,18] [--depths 0,4]
@@ -56,7 +56,10 @@ def main():
                 torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / args.reps
             leaves = n << levels
-            lookups = leaves * 490 if d in (0, 4) else None
+            D = d or 4  # the automatic depth of this shape
+            # per 2^D tree leaves: (levels - D) walk + 2^(D+1) - 2 tree + 2^D value AES
+            aes = ((levels - D) + (1 << (D + 1)) - 2 + (1 << D)) / (1 << D) if D > 0 else None
+            lookups = leaves * 160 * aes if aes else None
             frac = lookups / (ms / 1e3) / (256 * 32 * 2.4e9) if lookups else None
             print("roots 2^%d depth %s: %.3f ms, %.2f ns per tree leaf%s" % (
                 lr, d or "auto", ms, ms * 1e6 / leaves,
