@@ -52,6 +52,32 @@ struct PairMaskedKeys {
   }
 };
 
+// Progress-ordered wave priority for the lane-per-point walks (A/B:
+// DPF_WALK_PRIO=1): the sequencer serves a SIMD's older waves first, so the
+// waves of a round of blocks finish one after another and the last ones run
+// below the occupancy the LDS needs.  A wave starts at priority 3 and steps
+// down one level per quarter of its levels, so the waves behind are served
+// first (the same scheme as KExpand's DPF_EXPAND_PRIO).
+#ifndef DPF_WALK_PRIO
+#define DPF_WALK_PRIO 0
+#endif
+__device__ __forceinline__ void WalkPrio(int level, int num_levels) {
+  if constexpr (DPF_WALK_PRIO != 0) {
+    if (num_levels < 8) return;
+    const int q = (level * 4) / num_levels;  // wave-uniform
+    if (level > 0 && q != ((level - 1) * 4) / num_levels) {
+      if (q == 1)
+        __builtin_amdgcn_s_setprio(2);
+      else if (q == 2)
+        __builtin_amdgcn_s_setprio(1);
+      else
+        __builtin_amdgcn_s_setprio(0);
+    } else if (level == 0) {
+      __builtin_amdgcn_s_setprio(3);
+    }
+  }
+}
+
 // NP points of one thread: their indices, the index of their per-seed (or
 // per-key) inputs, and the walk state.
 template <int NP>
@@ -94,6 +120,7 @@ __device__ __forceinline__ void WalkPoints(const WalkArgs& w, Walk<NP>& s, const
     }
   }
   for (int level = 0; level < w.num_levels; ++level) {
+    WalkPrio(level, w.num_levels);
     const int bi = w.num_levels - level - 1 + w.rightshift;
     uint32_t bit[NP], mask[NP];
     Cw cw[NP];
