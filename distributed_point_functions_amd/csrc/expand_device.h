@@ -249,14 +249,19 @@ constexpr bool kStaged = kStagedEm<Em> && (1 << D) >= DPF_STAGE_LEAVES;
 
 // Leaf j of the lane's subtree (j wave-uniform): staged when the emitter
 // writes packed 16-byte leaves, flushed as one burst per DPF_STAGE_LEAVES.
-// Progress-ordered wave priority (A/B: DPF_EXPAND_PRIO=1).  The sequencer
-// favours older waves, so within a round of resident blocks the oldest waves
-// run ahead and finish first, and the last ones run alone at an occupancy
-// too low to keep the LDS busy.  A wave starts at priority 3 and steps down
-// one level per quarter of its subtree's leaves, so waves that are behind
-// are served first and a round's waves finish together.
+// Progress-ordered wave priority.  The sequencer favours older waves, so
+// within a round of resident blocks the oldest waves run ahead and finish
+// first, and the last ones run alone at an occupancy too low to keep the
+// LDS busy (tools/expand_trace.py: one round's waves ended between 78 and
+// 162 us, four per SIMD one after another).  A wave starts at priority 3 and
+// steps down one level per quarter of its subtree's leaves, so waves that
+// are behind are served first and a round's waves finish together (122-150
+// us).  Measured: one rank's c5 slice at N = 8 19.77-19.99 -> 19.28-19.36
+// ms, the whole c5 domain 153.9-154.1 -> 152.7-153.1 ms, c3's launch shape
+// -5 % (profiles/c5_slice_prio_r06/, ab_expand_prio_r06t/, r06u/).
+// DPF_EXPAND_PRIO=0 turns it off, 2 steps at 3/4, 7/8 and 15/16 instead.
 #ifndef DPF_EXPAND_PRIO
-#define DPF_EXPAND_PRIO 0
+#define DPF_EXPAND_PRIO 1
 #endif
 template <int D>
 __device__ __forceinline__ void ProgressPrio(int j) {

@@ -52,14 +52,15 @@ struct PairMaskedKeys {
   }
 };
 
-// Progress-ordered wave priority for the lane-per-point walks (A/B:
-// DPF_WALK_PRIO=1): the sequencer serves a SIMD's older waves first, so the
-// waves of a round of blocks finish one after another and the last ones run
-// below the occupancy the LDS needs.  A wave starts at priority 3 and steps
-// down one level per quarter of its levels, so the waves behind are served
-// first (the same scheme as KExpand's DPF_EXPAND_PRIO).
+// Progress-ordered wave priority for the lane-per-point walks: the
+// sequencer serves a SIMD's older waves first, so the waves of a round of
+// blocks finish one after another and the last ones run below the occupancy
+// the LDS needs.  A wave starts at priority 3 and steps down one level per
+// quarter of its levels, so the waves behind are served first (the scheme of
+// KExpand's DPF_EXPAND_PRIO).  c2's batched 64-key launch 1.587-1.600 ->
+// 1.555-1.577 ms (profiles/ab_walk_prio_r06x/); DPF_WALK_PRIO=0 turns it off.
 #ifndef DPF_WALK_PRIO
-#define DPF_WALK_PRIO 0
+#define DPF_WALK_PRIO 1
 #endif
 __device__ __forceinline__ void WalkPrio(int level, int num_levels) {
   if constexpr (DPF_WALK_PRIO != 0) {
