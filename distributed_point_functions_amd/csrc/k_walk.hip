@@ -62,6 +62,9 @@ struct PairMaskedKeys {
 #ifndef DPF_WALK_PRIO
 #define DPF_WALK_PRIO 1
 #endif
+#ifndef DPF_DCF_PRIO
+#define DPF_DCF_PRIO 1  // the same per hierarchy level in KDcfEvaluateDirect
+#endif
 __device__ __forceinline__ void WalkPrio(int level, int num_levels) {
   if constexpr (DPF_WALK_PRIO != 0) {
     if (num_levels < 8) return;
@@ -525,6 +528,7 @@ __global__ __launch_bounds__(kDcfBlockOf<BN>, kDcfWavesOf<BN>) void KDcfEvaluate
     for (int s = 0; s < vt.ns; ++s) acc[s] = 0;
     int level = 0;
     for (int h = 0; h < H; ++h) {
+      if (DPF_DCF_PRIO) WalkPrio(h, H);
       const int stop = a.tree_of[h];
       for (; level < stop; ++level) {
         const uint32_t bit = PathBit(p, H - 1 - level);
