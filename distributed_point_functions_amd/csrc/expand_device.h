@@ -12,7 +12,7 @@
 #include "aes_device.h"
 
 #ifndef DPF_EXPAND_EXTRA_DEPTHS
-#define DPF_EXPAND_EXTRA_DEPTHS 0  // KExpand<3>, <5> for A/B builds
+#define DPF_EXPAND_EXTRA_DEPTHS 0  // KExpand<3> for A/B builds
 #endif
 
 #ifndef DPF_EXPAND_MAX_GRID
@@ -813,7 +813,8 @@ int LaunchExpandCoop(hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
   return LaunchCheck("expand kernel launch");
 }
 
-// D >= 0: KExpand with DFS depth D; D = -1 / -2 / -3: KExpandCoop with E = 0 / 1 / -2.
+// D in {0, 1, 2, 4, 5, 6, 8}: KExpand with DFS depth D; D = -1 / -2 / -3:
+// KExpandCoop with E = 0 / 1 / -2.
 template <class Em>
 int LaunchExpandAnyD(int D, int grid, hipStream_t st, const ExpandArgs& a, const VtDev& vt) {
   if (D == -1) return LaunchExpandCoop<0, Em>(st, a, vt);
@@ -828,13 +829,13 @@ int LaunchExpandAnyD(int D, int grid, hipStream_t st, const ExpandArgs& a, const
       return LaunchExpand<2, Em>(grid, st, a, vt);
     case 4:
       return LaunchExpand<4, Em>(grid, st, a, vt);
+    case 5:
+      return LaunchExpand<5, Em>(grid, st, a, vt);
     case 6:
       return LaunchExpand<6, Em>(grid, st, a, vt);
 #if DPF_EXPAND_EXTRA_DEPTHS  // A/B builds only (tools/ab_c3_depth.sh)
     case 3:
       return LaunchExpand<3, Em>(grid, st, a, vt);
-    case 5:
-      return LaunchExpand<5, Em>(grid, st, a, vt);
 #endif
     default:
       return LaunchExpand<8, Em>(grid, st, a, vt);

@@ -17,8 +17,8 @@
 #include "kernel_args.h"
 #include "host_device.h"
 
-// D = 3 and 5 for the KExpand depth A/B (tools/ab_c3_depth.sh); the product
-// build instantiates D in {0, 1, 2, 4, 6, 8}.
+// D = 3 for the KExpand depth A/B (tools/ab_c3_depth.sh); the product build
+// instantiates D in {0, 1, 2, 4, 5, 6, 8}.
 #ifndef DPF_EXPAND_EXTRA_DEPTHS
 #define DPF_EXPAND_EXTRA_DEPTHS 0
 #endif
@@ -330,6 +330,12 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
   const int64_t range = leaf_end - leaf_begin;
   if (D == 8 && (range >> 8) < (int64_t{1} << 17)) D = 4;
   if (D == 4 && (range >> 4) < (int64_t{1} << 16)) D = 2;
+  // From 2^18 threads at D = 5 (one full round of resident blocks) the
+  // shallower walk beats D = 4's two rounds: c3's 2^16 prefix roots x 7
+  // levels 0.290-0.292 -> 0.271-0.274 ms, 2^17 roots 0.519-0.527 ->
+  // 0.480-0.483 ms; 2^15 roots (half a round) stay at D = 4 (0.160 against
+  // 0.177; profiles/ab_c3_depth5_r06/, with the wave priority).
+  if (D == 4 && num_levels >= 5 && (range >> 5) >= (int64_t{1} << 18)) D = 5;
   // Below 2^25 tree leaves the cooperative kernel computes every tree node
   // once per block instead of one root walk per thread (KExpandCoop,
   // expand_device.h): D = -1 (1024 leaves per block) or -2 (2048).
@@ -450,9 +456,9 @@ int dpf_amd_expand_and_correct_batched(int64_t num_keys, const void* root_seeds,
 }
 
 int dpf_amd_set_expand_depth(int depth) {
-  const bool extra = DPF_EXPAND_EXTRA_DEPTHS && (depth == 3 || depth == 5);
-  if (depth != 0 && depth != 1 && depth != 2 && depth != 4 && depth != 6 && depth != 8 &&
-      depth != -1 && depth != -2 && depth != -3 && !extra)
+  const bool extra = DPF_EXPAND_EXTRA_DEPTHS && depth == 3;
+  if (depth != 0 && depth != 1 && depth != 2 && depth != 4 && depth != 5 && depth != 6 &&
+      depth != 8 && depth != -1 && depth != -2 && depth != -3 && !extra)
     return -99;
   const int old = t_expand_depth;
   t_expand_depth = depth;

@@ -135,7 +135,7 @@ class forced_expand_depth:
     def __enter__(self):
         prev = _lib.lib().dpf_amd_set_expand_depth(self.depth)
         if prev == -99:
-            raise ValueError("expand depth must be 0, 1, 2, 4, 6, 8, -1, -2 or -3")
+            raise ValueError("expand depth must be 0, 1, 2, 4, 5, 6, 8, -1, -2 or -3")
         self.prev = prev
         return self
 

@@ -170,7 +170,7 @@ int dpf_amd_expand_and_correct_batched(
     void* out, void* stream);
 
 /* Testing knob (calling thread only): forces the register-DFS depth D of the
- * fused expansion kernel KExpand to 1, 2, 4 or 8 whenever num_levels >= D,
+ * fused expansion kernel KExpand to 1, 2, 4, 5, 6 or 8 whenever num_levels >= D,
  * or the cooperative kernel KExpandCoop with 1024 (-1), 2048 (-2) or 256 (-3)
  * leaves per block whenever num_levels >= 10 / 11 / 8, so the kernels that
  * other launch sizes select can be checked on small domains.  0 restores the

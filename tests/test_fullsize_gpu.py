@@ -98,12 +98,12 @@ def _assert_host_layout_equals_words(spec, got: np.ndarray, words: np.ndarray, w
 # Every DFS depth, every value type, whole domain vs oracle
 # ---------------------------------------------------------------------------
 
-@pytest.mark.parametrize("depth", [1, 2, 4, 6, 8])
+@pytest.mark.parametrize("depth", [1, 2, 4, 5, 6, 8])
 @pytest.mark.parametrize("spec", TYPES, ids=[repr(t) for t in TYPES])
 def test_forced_depth_matches_oracle(K, cuda, spec, depth):
     """Every DFS depth KExpand is instantiated with, every emitter (D = 6
     included: the batched PIR selection's depth, instantiated for every
-    type since round 6)."""
+    type since round 6; D = 5: c3's levels and 2^23-2^24-leaf expansions)."""
     d, k0, k1, alpha, beta = _keys(spec, 14, seed=depth)
     assert d.hierarchy_to_tree(0) >= depth
     with K.forced_expand_depth(depth):
@@ -116,7 +116,7 @@ def test_forced_depth_matches_oracle(K, cuda, spec, depth):
 RANGE_TYPES = [C5, ("int", 64), ("xor", 128)]
 
 
-@pytest.mark.parametrize("depth", [4, 6, 8])
+@pytest.mark.parametrize("depth", [4, 5, 6, 8])
 @pytest.mark.parametrize("spec", RANGE_TYPES, ids=[repr(t) for t in RANGE_TYPES])
 def test_forced_depth_leaf_ranges(K, cuda, spec, depth):
     """Ragged leaf ranges that start and end inside a 2^D-leaf subtree, both

@@ -363,7 +363,7 @@ def test_size_query_validates_prefixes(api):
         assert n.value == len(ok) * 256
 
 
-@pytest.mark.parametrize("depth", [4, 6, 8])
+@pytest.mark.parametrize("depth", [4, 5, 6, 8])
 def test_incremental_levels_under_forced_depth(api, depth):
     """The device incremental path (dpf.cc EvaluateUntilOnDevice: 7 tree
     levels below each prefix root for uint64 at 8-bit hierarchy steps, c3's
