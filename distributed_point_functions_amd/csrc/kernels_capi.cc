@@ -90,9 +90,16 @@ constexpr int64_t kCoopMaxLeaves = int64_t{1} << 22;
 // bound against KExpand<4> 1.32 and the cooperative 1.42; 16 x 2^19 0.377
 // vs 0.392), else KExpand<4>; KExpandCoop with per-block keys below (8 x
 // 2^19: 0.212 vs D = 4 0.224, D = 6 0.379; 100 x 2^16: 0.316 vs 0.368).
+// Depth of a batched expansion: the deepest DFS that still fills one round
+// of resident blocks (2^18 threads) — D = 6 from 2^24 leaves in total for
+// the 16-byte selection type, D = 5 from 2^23 — else D = 4 or the
+// cooperative kernel.  With the wave priority on, 16 keys x 2^19 leaves
+// (2^23): D = 4 / 5 / 6 0.360 / 0.305 / 0.347 ms; 64 x 2^19: 1.267 / 1.080 /
+// 1.032 ms (profiles/sweep_batched_r06.log).
 int BatchedDepth(int64_t num_keys, int64_t range, bool wide) {
   const int64_t total = num_keys * range;
-  if (total >= (int64_t{1} << 23) && range >= 64 && wide) return 6;
+  if (total >= (int64_t{1} << 24) && range >= 64 && wide) return 6;
+  if (total >= (int64_t{1} << 23) && range >= 32) return 5;
   if (total >= (int64_t{1} << 23) && range >= 16) return 4;
   return CoopDepth(total);
 }

@@ -468,7 +468,7 @@ def test_c5_eight_rank_split_reproduces_one_rank(K, cuda, c5_full):
         assert _chunked_equal(buf, full), world
 
 
-@pytest.mark.parametrize("variant", [0, 2, 4, 6, 8, -1, -2, -3])
+@pytest.mark.parametrize("variant", [0, 2, 4, 5, 6, 8, -1, -2, -3])
 @pytest.mark.parametrize("spec,ld", [(("xor", 128), 14), (("int", 64), 15), (("int", 32), 16),
                                      (("int", 8), 18), (C5, 13)])
 def test_batched_keys_match_oracle(K, cuda, spec, ld, variant):

@@ -1,6 +1,6 @@
 """Expansion kernel variants across launch sizes (single key and batched
 keys) on one MI355X: kernel time per forced variant (dpf_amd_set_expand_depth:
-D = 1/2/4/8 KExpand, -1/-2/-3 KExpandCoop E = 0/1/-2, 0 automatic), HIP events on the
+D = 1/2/4/5/6/8 KExpand, -1/-2/-3 KExpandCoop E = 0/1/-2, 0 automatic), HIP events on the
 launch stream.  XorWrapper<uint128> (the PIR selection type) and uint64 (c1).
 
     python tools/expand_sweep.py [single|batched]
@@ -41,7 +41,7 @@ if mode == "single":
         cepb = 1 << (ld - L)
         out = torch.empty((1 << L) * cepb * desc.out_stride, dtype=torch.uint8, device=dev)
         res = {}
-        for D in (2, 4, 8, -3, -1, -2, 0):  # the automatic choice last (warm clocks)
+        for D in (2, 4, 5, 8, -3, -1, -2, 0):  # the automatic choice last (warm clocks)
             def step():
                 kernels.expand_and_correct(kd["seed"], kd["cb"], L, kd["cw"], kd["ccl"], kd["ccr"],
                                            desc, kd["corr"], kd["party"], cepb, 0, 1 << L, out)
@@ -65,7 +65,7 @@ else:
         parties = [k["party"] for k in kd]
         out = torch.empty(q * leaves * 16, dtype=torch.uint8, device=dev)
         res = {}
-        for D in (2, 4, 6, 8, -3, -1, -2, 0):  # the automatic choice last (warm clocks)
+        for D in (2, 4, 5, 6, 8, -3, -1, -2, 0):  # the automatic choice last (warm clocks)
             def step():
                 kernels.expand_and_correct_batched(seeds, cbs, L, cws, ccl, ccr, desc, corr,
                                                    parties, 1, 0, leaves, out)
