@@ -335,7 +335,13 @@ int dpf_amd_expand_and_correct(int64_t num_roots, const void* root_seeds,
   // 2^24 tree leaves D = 8 1.32 ms vs D = 4 0.80; 2^25: 1.33 vs 1.46), and
   // D = 4 needs 2^16 (2^19 tree leaves: D = 2 0.059 ms vs D = 4 0.112).
   const int64_t range = leaf_end - leaf_begin;
-  if (D == 8 && (range >> 8) < (int64_t{1} << 17)) D = 4;
+  // With the wave priority, the deepest DFS whose threads still fill one
+  // round of resident blocks (2^18 threads) wins: D = 8 from 2^26 tree
+  // leaves, D = 6 from 2^24 (uint64, 2^25 leaves: D = 4 / 5 / 6 / 8 1.33 /
+  // 1.11 / 1.03 / 1.26 ms; 2^24: 0.77 / 0.59 / 0.53 / 1.24; 2^26: D = 6 2.07,
+  // D = 8 2.00; profiles/sweep_large_r06.log).
+  if (D == 8 && (range >> 8) < (int64_t{1} << 18))
+    D = (range >> 6) >= (int64_t{1} << 18) ? 6 : 4;
   if (D == 4 && (range >> 4) < (int64_t{1} << 16)) D = 2;
   // From 2^18 threads at D = 5 (one full round of resident blocks) the
   // shallower walk beats D = 4's two rounds: c3's 2^16 prefix roots x 7

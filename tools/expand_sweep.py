@@ -3,7 +3,7 @@ keys) on one MI355X: kernel time per forced variant (dpf_amd_set_expand_depth:
 D = 1/2/4/5/6/8 KExpand, -1/-2/-3 KExpandCoop E = 0/1/-2, 0 automatic), HIP events on the
 launch stream.  XorWrapper<uint128> (the PIR selection type) and uint64 (c1).
 
-    python tools/expand_sweep.py [single|batched]
+    python tools/expand_sweep.py [single|large|batched]
 """
 import json
 import os
@@ -30,18 +30,23 @@ def keyset(ld, vt, q):
     return dpf, kd
 
 
-if mode == "single":
-    for vt, ld in [(V.Integer(64), 12), (V.Integer(64), 16), (V.XorWrapper(128), 16),
-                   (V.Integer(64), 17), (V.Integer(64), 18), (V.Integer(64), 20),
-                   (V.XorWrapper(128), 19), (V.Integer(64), 22), (V.Integer(64), 24),
-                   (V.XorWrapper(128), 24)]:
+if mode in ("single", "large"):
+    cases = [(V.Integer(64), 12), (V.Integer(64), 16), (V.XorWrapper(128), 16),
+             (V.Integer(64), 17), (V.Integer(64), 18), (V.Integer(64), 20),
+             (V.XorWrapper(128), 19), (V.Integer(64), 22), (V.Integer(64), 24),
+             (V.XorWrapper(128), 24)]
+    if mode == "large":  # 2^24-2^28 tree leaves: D = 4 / 5 / 6 / 8 around the D = 8 threshold
+        cases = [(V.Integer(64), 25), (V.Integer(64), 26), (V.Integer(64), 27),
+                 (V.Integer(64), 28), (V.Integer(64), 29)]
+    for vt, ld in cases:
         dpf, (kd,) = keyset(ld, vt, 1)
         desc = dpf.value_type_descriptor(0)
         L = kd["L"]
         cepb = 1 << (ld - L)
         out = torch.empty((1 << L) * cepb * desc.out_stride, dtype=torch.uint8, device=dev)
         res = {}
-        for D in (2, 4, 5, 8, -3, -1, -2, 0):  # the automatic choice last (warm clocks)
+        depths = (4, 5, 6, 8, 0) if mode == "large" else (2, 4, 5, 8, -3, -1, -2, 0)
+        for D in depths:  # the automatic choice last (warm clocks)
             def step():
                 kernels.expand_and_correct(kd["seed"], kd["cb"], L, kd["cw"], kd["ccl"], kd["ccr"],
                                            desc, kd["corr"], kd["party"], cepb, 0, 1 << L, out)
