@@ -1608,7 +1608,28 @@ Status EvaluateUntilOnDevice(const DpfState& st, int hierarchy_level,
   trace.Mark("setup");
   int* flags = reinterpret_cast<int*>(w + o_flags);
   DPF_RETURN_IF_ERROR(HipStatus(hipMemsetAsync(flags, 0, sizeof(int), s), "hipMemsetAsync"));
-  DPF_RETURN_IF_ERROR(ThreadUploadRing().Copy(w + o_p, prefixes.data(), 16 * size_t(n), s));
+  // The prefixes are written by the host straight into fine-grained device
+  // memory (large-BAR devices, UploadRing::Place) and read there by the
+  // de-duplication, in place of a pinned-slot memcpy, a copy kernel and its
+  // dependent-dispatch gap (~60 us of a c3 level): c3's 16 levels 6.43-6.93
+  // -> 6.14-6.26 ms (profiles/ab_place_prefixes_r06/).  DPF_AMD_PLACE_PREFIXES=0
+  // keeps the copy (A/B); devices without the host-write path copy anyway.
+  static const bool place_prefixes = [] {
+    const char* e = std::getenv("DPF_AMD_PLACE_PREFIXES");
+    return !(e != nullptr && std::strcmp(e, "0") == 0);
+  }();
+  bool pplaced = false;
+  int pslot = -1;
+  char* pdev = nullptr;
+  if (place_prefixes) {
+    const UploadRing::HostPart pp{prefixes.data(), 16 * size_t(n)};
+    const size_t off0 = 0;
+    DPF_RETURN_IF_ERROR(
+        ThreadUploadRing().Place(&pp, 1, 16 * size_t(n), &off0, &pplaced, &pslot, &pdev));
+  }
+  const char* pref = pplaced ? pdev : w + o_p;
+  if (!pplaced)
+    DPF_RETURN_IF_ERROR(ThreadUploadRing().Copy(w + o_p, prefixes.data(), 16 * size_t(n), s));
   DPF_RETURN_IF_ERROR(ThreadUploadRing().CopyPacked(w + o_cw, parts, 9, cw_bytes, coff, s));
   trace.Mark("upload");
   const uint64_t limit[2] = {prev_ld < 64 ? (uint64_t{1} << prev_ld) : 0,
@@ -1616,7 +1637,7 @@ Status EvaluateUntilOnDevice(const DpfState& st, int hierarchy_level,
   int32_t* pidx = reinterpret_cast<int32_t*>(w + o_idx);
   uint8_t* plow = reinterpret_cast<uint8_t*>(w + o_low);
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd::DedupPrefixes(
-      w + o_p, n, bbits, prev_ld < 128 ? limit : nullptr, pidx, plow, next->prefixes(),
+      pref, n, bbits, prev_ld < 128 ? limit : nullptr, pidx, plow, next->prefixes(),
       next->count_dev(), reinterpret_cast<int64_t*>(w + o_blk), flags, s)));
   const uint64_t root[2] = {ctx.key().seed().low(), ctx.key().seed().high()};
   DPF_RETURN_IF_ERROR(AbiStatus(dpf_amd::LookupPartialEvaluations(
@@ -1647,6 +1668,7 @@ Status EvaluateUntilOnDevice(const DpfState& st, int hierarchy_level,
       reinterpret_cast<const uint8_t*>(w + o_cw + coff[8]), &vt,
       reinterpret_cast<const uint64_t*>(corr.data()), ctx.key().party(), cepb, 0, n << down,
       final_dev, s)));
+  if (pplaced) DPF_RETURN_IF_ERROR(ThreadUploadRing().ReleasePlaced(pslot, s));
   DPF_RETURN_IF_ERROR(CopyToHost(readback, flags, sizeof(int), s));
   DPF_RETURN_IF_ERROR(CopyToHost(readback + 1, next->count_dev(), sizeof(int64_t), s));
   trace.Mark("launch");

@@ -783,7 +783,7 @@ class UploadRing {
   };
   Slot slots_[kSlots];
   int next_ = 0;
-  static constexpr size_t kMaxPlaceBytes = size_t{64} << 10;
+  static constexpr size_t kMaxPlaceBytes = size_t{1} << 20;  // c3's 2^16 prefixes
   struct PlaceSlot {
     void* dev = nullptr;  // fine-grained device memory, written by the host
     size_t cap = 0;
