@@ -1625,7 +1625,8 @@ Status EvaluateUntilOnDevice(const DpfState& st, int hierarchy_level,
     const UploadRing::HostPart pp{prefixes.data(), 16 * size_t(n)};
     const size_t off0 = 0;
     DPF_RETURN_IF_ERROR(
-        ThreadUploadRing().Place(&pp, 1, 16 * size_t(n), &off0, &pplaced, &pslot, &pdev));
+        ThreadUploadRing().Place(&pp, 1, 16 * size_t(n), &off0, &pplaced, &pslot, &pdev,
+                                 UploadRing::kMaxPlaceLargeBytes));
   }
   const char* pref = pplaced ? pdev : w + o_p;
   if (!pplaced)

@@ -711,10 +711,12 @@ class UploadRing {
   // s) must follow the last launch that reads the slot.  *placed = false
   // (nothing done) when the device is not large-BAR, the one-time check of
   // the path failed, DPF_AMD_HOST_WRITE=0, or the parts exceed a slot.
+  // `max_bytes`: the largest upload placed (default: small key parts; c3's
+  // prefix lists pass kMaxPlaceLargeBytes).
   Status Place(const HostPart* parts, int k, size_t bytes, const size_t* off, bool* placed,
-               int* slot, char** dev) {
+               int* slot, char** dev, size_t max_bytes = kMaxPlaceBytes) {
     *placed = false;
-    if (bytes == 0 || bytes > kMaxPlaceBytes) return OkStatus();
+    if (bytes == 0 || bytes > max_bytes) return OkStatus();
     int d = 0;
     DPF_RETURN_IF_ERROR(HipStatus(hipGetDevice(&d), "hipGetDevice"));
     if (!HostWritable(d)) return OkStatus();
@@ -783,7 +785,12 @@ class UploadRing {
   };
   Slot slots_[kSlots];
   int next_ = 0;
-  static constexpr size_t kMaxPlaceBytes = size_t{1} << 20;  // c3's 2^16 prefixes
+  static constexpr size_t kMaxPlaceBytes = size_t{64} << 10;
+
+ public:
+  static constexpr size_t kMaxPlaceLargeBytes = size_t{1} << 20;  // c3's 2^16 prefixes
+
+ private:
   struct PlaceSlot {
     void* dev = nullptr;  // fine-grained device memory, written by the host
     size_t cap = 0;
